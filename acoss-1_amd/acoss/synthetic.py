@@ -1,0 +1,102 @@
+"""Synthetic HPCP-like cover-song corpora (SURVEY.md §8d "Synthetic inputs").
+
+There is no network and no audio in this environment, so benchmarks and end-to-end tests
+run on seeded synthetic 12-d chroma with the clique structure of the real datasets:
+
+* per clique a base sequence: a random walk over the 24 major/minor triad templates
+  (dwell ~U[8, 64] frames) plus |N(0, 0.1)| noise, non-negative, unit-max per frame
+  (like essentia HPCP), with 2 % silent (all-zero) frames;
+* every cover = the base rolled by a random key k in [0, 12), time-stretched by
+  U[0.8, 1.25] (nearest-index resampling), fresh noise, renormalised; float32 (n, 12).
+
+Clique shapes: covers80 (164 tracks: 77x2, 2x3, 1x4, from acoss/data/covers80_annotations.csv)
+and Da-TACOS benchmark (1000x13 + 2000 singletons = 15,000 tracks).
+"""
+import os
+
+import numpy as np
+
+SEED = 20250101
+_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+
+
+def triad_templates():
+    """(24, 12) major + minor triads, unit max."""
+    T = np.zeros((24, 12), np.float32)
+    for r in range(12):
+        T[r, [r, (r + 4) % 12, (r + 7) % 12]] = 1.0
+        T[12 + r, [r, (r + 3) % 12, (r + 7) % 12]] = 1.0
+    return T
+
+
+def _unitmax(x):
+    mx = x.max(axis=1, keepdims=True)
+    return np.where(mx > 0, x / np.where(mx > 0, mx, 1), 0).astype(np.float32)
+
+
+def base_sequence(rng, n, silence=0.02):
+    T = triad_templates()
+    out = np.empty((n, 12), np.float32)
+    i = 0
+    while i < n:
+        dwell = int(rng.integers(8, 65))
+        out[i:i + dwell] = T[rng.integers(0, 24)]
+        i += dwell
+    return out
+
+
+def render(rng, base, silence=0.02):
+    x = base + np.abs(rng.normal(0.0, 0.1, base.shape)).astype(np.float32)
+    x = _unitmax(x)
+    x[rng.random(len(x)) < silence] = 0.0
+    return x
+
+
+def cover_of(rng, base, n_out=None, stretch=(0.8, 1.25)):
+    k = int(rng.integers(0, 12))
+    s = float(rng.uniform(*stretch))
+    n = n_out if n_out is not None else max(16, int(round(len(base) * s)))
+    idx = np.minimum((np.arange(n) * (len(base) / n)).astype(np.int64), len(base) - 1)
+    return np.roll(base[idx], k, axis=1)
+
+
+def clique_sizes(shape):
+    if shape == "covers80":
+        import pandas as pd
+        df = pd.read_csv(os.path.join(_DATA, "covers80_annotations.csv"), dtype=str)
+        return [int(c) for c in df.groupby("work_id", sort=False).size().values]
+    if shape == "datacos":
+        return [13] * 1000 + [1] * 2000
+    raise ValueError(shape)
+
+
+def make_corpus(shape="covers80", frames=2000, frames_jitter=0.0, seed=SEED, stretch=True):
+    """Return (tracks: list of (n_i, 12) float32, labels: int array).
+
+    frames: length of every base sequence (the CSM input length); with
+    stretch=True covers are resampled to U[0.8,1.25]x that length, else all tracks have
+    exactly `frames` frames. frames_jitter: base length ~ U[1-j, 1+j] * frames.
+    """
+    rng = np.random.Generator(np.random.PCG64(seed))
+    tracks, labels = [], []
+    for lab, size in enumerate(clique_sizes(shape)):
+        n0 = frames if frames_jitter <= 0 else int(round(frames * rng.uniform(1 - frames_jitter, 1 + frames_jitter)))
+        base = base_sequence(rng, n0)
+        for v in range(size):
+            if v == 0:
+                seq = base
+            else:
+                seq = cover_of(rng, base, None if stretch else n0)
+            tracks.append(render(rng, seq))
+            labels.append(lab)
+    return tracks, np.asarray(labels, np.int32)
+
+
+def pack(tracks):
+    """List of (n_i, 12) -> (feats (sum n, 12) f32, off int64, len int32)."""
+    lens = np.array([len(t) for t in tracks], np.int32)
+    off = np.zeros(len(tracks), np.int64)
+    if len(tracks) > 1:
+        off[1:] = np.cumsum(lens[:-1])
+    feats = np.ascontiguousarray(np.concatenate(tracks, 0), np.float32) if tracks else np.zeros((0, 12), np.float32)
+    return feats, off, lens

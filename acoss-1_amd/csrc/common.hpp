@@ -1,0 +1,104 @@
+// common.hpp — host + device helpers shared by the acoss HIP kernels (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "acoss_hip.h"
+
+namespace acoss {
+
+// ---- host side: error string + workspace cache (common.cpp) ----
+void set_error(const char* fmt, ...);
+void clear_error();
+// Grow-only device buffer `slot` on the current device (stream-ordered users: the previous
+// contents are not preserved on growth). Returns nullptr (and sets the error) on failure.
+void* workspace(int slot, size_t bytes);
+int release_all_workspaces();
+
+#define ACOSS_HIP_CHECK(expr)                                                                      \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess) {                                                                        \
+      ::acoss::set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr, hipGetErrorString(e_));        \
+      return ACOSS_E_HIP;                                                                          \
+    }                                                                                              \
+  } while (0)
+
+#define ACOSS_LAUNCH_CHECK()                                                                       \
+  do {                                                                                             \
+    hipError_t e_ = hipGetLastError();                                                             \
+    if (e_ != hipSuccess) {                                                                        \
+      ::acoss::set_error("%s:%d kernel launch: %s", __FILE__, __LINE__, hipGetErrorString(e_));    \
+      return ACOSS_E_HIP;                                                                          \
+    }                                                                                              \
+  } while (0)
+
+// essentia stackChromaFrames count: for (i = 0; i < n - m*tau; i += tau).
+__host__ __device__ inline int stacked_len(int n, int m, int tau) {
+  const int inc = m * tau;
+  return (n <= inc || tau <= 0) ? 0 : (n - inc + tau - 1) / tau;
+}
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---- device helpers ----
+constexpr int kWave = 64;
+
+__device__ inline float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+__device__ inline double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+
+__device__ inline int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ inline unsigned wave_min_u32(unsigned v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o));
+  return v;
+}
+
+// Inclusive scan over the 64 lanes of a wave.
+__device__ inline int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// Correctly rounded sqrt (hipcc default: -fhip-fp32-correctly-rounded-divide-sqrt).
+__device__ inline float sqrt_rn(float x) { return __builtin_sqrtf(x); }
+
+// Largest float T such that sqrt_rn(T) <= thr (thr >= 0). sqrt_rn is monotone, so for a
+// key k >= 0:  sqrt_rn(k) <= thr  <=>  k <= T.  Lets the mask compare squared distances.
+__host__ __device__ inline float next_up(float x) {
+  unsigned u = __builtin_bit_cast(unsigned, x);
+  return __builtin_bit_cast(float, u + 1u);  // x >= 0, finite
+}
+__host__ __device__ inline float next_down(float x) {
+  unsigned u = __builtin_bit_cast(unsigned, x);
+  return u == 0u ? x : __builtin_bit_cast(float, u - 1u);
+}
+__device__ inline float sq_threshold(float thr) {
+  float t = thr * thr;
+  for (int it = 0; it < 16 && t > 0.0f && sqrt_rn(t) > thr; ++it) t = next_down(t);
+  for (int it = 0; it < 16 && sqrt_rn(next_up(t)) <= thr; ++it) t = next_up(t);
+  return t;
+}
+
+}  // namespace acoss

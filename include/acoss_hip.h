@@ -1,0 +1,124 @@
+/*
+ * acoss_hip.h — C-ABI of libacoss_hip.so, the MI355X (gfx950) engine for the acoss
+ * all-pairs cross-similarity + alignment hot path.
+ *
+ * Conventions:
+ *  - Every array pointer is a DEVICE pointer owned by the caller (torch tensors), unless
+ *    the parameter name ends in `_host`. Scalars are passed by value.
+ *  - Row-major, C-contiguous. Chroma features are packed: track t occupies rows
+ *    [track_off[t], track_off[t] + track_len[t]) of a (sum_len x 12) float32 block.
+ *  - Every call is stream-ordered on `hip_stream` (a hipStream_t; NULL = default stream)
+ *    and returns 0 on success or a negative ACOSS_E* code. No C++ exception crosses the
+ *    ABI; acoss_last_error() returns a thread-local message for the last failure.
+ *  - The only allocation is an internal, grow-only device workspace cache
+ *    (acoss_release_workspace() frees it).
+ *
+ * Each entry point cites the reference interface it replaces (paths relative to the
+ * reference repo silvadirceu/acoss-1).
+ */
+#ifndef ACOSS_HIP_H
+#define ACOSS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACOSS_OK 0
+#define ACOSS_E_ARG (-1)      /* invalid argument / unsupported parameter */
+#define ACOSS_E_SHAPE (-2)    /* track too short for the frame stacking (n <= m*tau) */
+#define ACOSS_E_HIP (-3)      /* HIP runtime error */
+#define ACOSS_E_NONBINARY (-4)/* non-binary element in an alignment input (alignment_tools.py:22-23) */
+
+/* Parameters of essentia ChromaCrossSimilarity + CoverSongSimilarity as acoss calls them
+ * (acoss/algorithms/rqa_serra09.py:31-32,60-64; latefusion_chen.py:58-71). */
+typedef struct acoss_crp_params {
+  int32_t m;          /* frameStackSize, default 9 */
+  int32_t tau;        /* frameStackStride, default 1 */
+  float kappa;        /* binarizePercentile, default 0.095 */
+  int32_t oti;        /* 1 = optimal transposition of the reference (default), 0 = none */
+  float gamma_open;   /* disOnset, default 0.5 */
+  float gamma_ext;    /* disExtension, default 0.5 */
+} acoss_crp_params;
+
+/* Library / build information. */
+const char* acoss_version(void);
+const char* acoss_last_error(void);
+int acoss_release_workspace(void);
+
+/* ---------------------------------------------------------------------------------
+ * Serra09 / LateFusionChen hot path for a batch of song pairs (A1/A4/A9/A10/A16).
+ * Replaces, per pair (i, j) = (pairs[2p], pairs[2p+1]):
+ *   crp = essentia.ChromaCrossSimilarity(frameStackSize=m, frameStackStride=tau,
+ *                                        binarizePercentile=kappa, oti=oti)(query, reference)
+ *   _, qmax = essentia.CoverSongSimilarity('serra09', 'symmetric')(crp)
+ *   _, dmax = essentia.CoverSongSimilarity('chen17',  'symmetric')(crp)
+ * at acoss/algorithms/rqa_serra09.py:55-69 and acoss/algorithms/latefusion_chen.py:58-73.
+ * query = track pairs[2p], reference = track pairs[2p+1]. qmax_out / dmax_out / oti_out are
+ * float[n_pairs] / float[n_pairs] / int32[n_pairs] and each may be NULL (not computed).
+ * max_len = max track_len over the tracks referenced (host scalar; sizes the workspace).
+ * --------------------------------------------------------------------------------- */
+int acoss_crp_align(const float* feats, const int64_t* track_off, const int32_t* track_len, int32_t n_tracks,
+                    int32_t max_len, const int32_t* pairs, int64_t n_pairs, const acoss_crp_params* params,
+                    float* qmax_out, float* dmax_out, int32_t* oti_out, void* hip_stream);
+
+/* Single-pair CRP with every intermediate exposed (parity / debugging of A1/A4).
+ * X: (M x 12), Y: (N x 12) device float32. Outputs (device, each may be NULL):
+ *   dist (Mp x Np) float32 stacked Euclidean distances, thr_row (Mp), thr_col (Np) float32
+ *   percentile thresholds, crp (Mp x Np) uint8 mutual-neighbour mask, oti (1) int32.
+ * Mp = ceil((M - m*tau)/tau), Np likewise (essentia stackChromaFrames). */
+int acoss_crp_pair(const float* X, int32_t M, const float* Y, int32_t N, const acoss_crp_params* params,
+                   float* dist, float* thr_row, float* thr_col, uint8_t* crp, int32_t* oti, void* hip_stream);
+
+/* essentia CoverSongSimilarity(alignmentType, distanceType='symmetric') on a given binary
+ * matrix (A9/A10): crp (M x N) uint8 in {0,1}. align = 0 'serra09' (Qmax), 1 'chen17'
+ * (dmax). score_out: float[1]. Replaces the alignment calls at rqa_serra09.py:64,67 and
+ * latefusion_chen.py:67-71 when the CRP comes from elsewhere. */
+int acoss_align_crp(const uint8_t* crp, int32_t M, int32_t N, int32_t align, float gamma_open, float gamma_ext,
+                    float* score_out, void* hip_stream);
+
+/* acoss smith_waterman_constrained (A8, acoss/algorithms/utils/alignment_tools.py:25-46) on
+ * a batch of binary matrices: matrix b is (rows[b] x cols[b]) uint8 at byte offset off[b]
+ * of `mats`. score_out: double[n_mats]. Bit-exact float64 (same evaluation order). */
+int acoss_sw_constrained(const uint8_t* mats, const int64_t* off, const int32_t* rows, const int32_t* cols,
+                         int32_t n_mats, int32_t max_rows, int32_t max_cols, double* score_out, void* hip_stream);
+
+/* Cross-similarity matrices (A5/A6/A2): acoss get_csm / get_csm_cosine
+ * (cross_recurrence.py:30-73), optionally after get_csm_blocked_oti's query rotation
+ * (:105-134): with oti_shift >= 0 every 12-bin block of each X row is rolled by oti_shift
+ * (np.roll on the chroma axis) first. X (M x d), Y (N x d) float32; out (M x N) float32.
+ * kind = 0 euclidean, 1 cosine, 2 self-similarity of X (get_ssm :10-28; Y ignored). */
+int acoss_csm(const float* X, int32_t M, const float* Y, int32_t N, int32_t d, int32_t kind, int32_t oti_shift,
+              float* out, void* hip_stream);
+
+/* acoss get_oti (cross_recurrence.py:75-103) for a batch: C1, C2 (n x 12) float32 global
+ * chroma vectors; out int32[n] = argmax_i sum(roll(C1[k], i) * C2[k]), first max wins. */
+int acoss_get_oti(const float* C1, const float* C2, int32_t n, int32_t* out, void* hip_stream);
+
+/* acoss csm_to_binary (A7, cross_recurrence.py:136-161): row-wise kappa nearest neighbours.
+ * D (M x N) float32 -> B (M x N) uint8. nneighbs = number of ones per row (the host computes
+ * int(np.round(kappa * N)) or kappa itself, as the reference does); nneighbs <= 0 -> all ones.
+ * Among equal distances the lowest column index wins (numpy's argpartition choice is
+ * arbitrary). */
+int acoss_binarize_rows(const float* D, int32_t M, int32_t N, int32_t nneighbs, uint8_t* B, void* hip_stream);
+
+/* acoss getWCSM (A14, similarity_fusion.py:38-54): W = exp(-CSM^2 / (2 (mu*Eps)^2)) with
+ * Eps = (rowmean_k2 + colmean_k1 + CSM)/3 of the k2 / k1 smallest per row / column.
+ * CSM, W: (M x N) float32. */
+int acoss_wcsm(const float* CSM, int32_t M, int32_t N, int32_t k1, int32_t k2, float mu, float* W,
+               void* hip_stream);
+
+/* SiMPle matrix profile score (A11, acoss/algorithms/simple_silva.py:68-118) for a batch of
+ * ordered pairs, including the per-pair OTI roll of the reference (Simple.oti, :45-54).
+ * feats: packed (12 x n_t) float64 blocks, track t at element offset track_off[t] (dim-major,
+ * as the reference's seq arrays). score_out[p] = median_i min_j dist (the reference stores
+ * -score, simple_silva.py:125). oti_out may be NULL. */
+int acoss_simple_mp(const double* feats, const int64_t* track_off, const int32_t* track_len, int32_t n_tracks,
+                    int32_t max_len, const int32_t* pairs, int64_t n_pairs, int32_t sslen, double* score_out,
+                    int32_t* oti_out, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACOSS_HIP_H */

@@ -1,0 +1,146 @@
+"""TEST INFRASTRUCTURE — the parity oracle. NOT part of the product.
+
+Only tests/, __graft_entry__.smoke() and bench.py's `cpu_baseline` leg may import this
+package, and only as the checker / timed CPU baseline. The product (acoss-1_amd/acoss)
+never imports it.
+
+* ``liboracle.so`` (crp_oracle.cpp): CPU restatement of the essentia CRP + Qmax/dmax path,
+  acoss smith_waterman_constrained and Simple.simple_sim. See the file header for the
+  canonical arithmetic and the reference file:line each function follows.
+* ``np_oracle``: numpy restatements of the acoss Python hot-path helpers
+  (cross_recurrence.py, similarity_fusion.getWCSM, simple_silva.oti), pinned against
+  tests/golden/reference_golden.npz (generated from the reference by
+  tests/golden/make_golden.py).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+_fp = ctypes.POINTER(ctypes.c_float)
+_dp = ctypes.POINTER(ctypes.c_double)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(_HERE, "crp_oracle.cpp")):
+            build()
+        L = ctypes.CDLL(LIB)
+        L.or_stacked_len.restype = ctypes.c_int
+        L.or_oti.restype = ctypes.c_int
+        L.or_percentile_sorted.restype = ctypes.c_float
+        L.or_percentile_sorted.argtypes = [_fp, ctypes.c_int, ctypes.c_float]
+        L.or_align.restype = ctypes.c_float
+        L.or_align.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_int]
+        L.or_crp_pair.restype = ctypes.c_int
+        L.or_crp_pair.argtypes = [_fp, ctypes.c_int, _fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                  ctypes.c_int, ctypes.c_float, ctypes.c_float, _fp, _fp, _i32p, _u8p, _fp, _fp]
+        L.or_crp_batch.restype = ctypes.c_int
+        L.or_crp_batch.argtypes = [_fp, _i64p, _i32p, _i32p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_float, ctypes.c_int, ctypes.c_float, ctypes.c_float, _fp, _fp, _i32p,
+                                   ctypes.c_int]
+        L.or_crp_dist.argtypes = [_fp, ctypes.c_int, _fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp]
+        L.or_sw_constrained.restype = ctypes.c_double
+        L.or_sw_constrained.argtypes = [_u8p, ctypes.c_int, ctypes.c_int]
+        L.or_simple_sim.restype = ctypes.c_double
+        L.or_simple_sim.argtypes = [_dp, ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int]
+        L.or_track_profile.argtypes = [_fp, ctypes.c_int, _fp]
+        L.or_oti.argtypes = [_fp, _fp]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def stacked_len(n, m=9, tau=1):
+    return lib().or_stacked_len(int(n), int(m), int(tau))
+
+
+def crp_pair(X, Y, m=9, tau=1, kappa=0.095, oti=True, gamma_open=0.5, gamma_ext=0.5):
+    """Whole Serra09/Chen path for one pair -> dict(qmax, dmax, oti, crp, thr_row, thr_col)."""
+    X = np.ascontiguousarray(X, np.float32)
+    Y = np.ascontiguousarray(Y, np.float32)
+    Mp, Np = stacked_len(len(X), m, tau), stacked_len(len(Y), m, tau)
+    if Mp <= 0 or Np <= 0:
+        raise ValueError("track too short for m=%d tau=%d" % (m, tau))
+    C = np.zeros((Mp, Np), np.uint8)
+    tr = np.zeros(Mp, np.float32)
+    tc = np.zeros(Np, np.float32)
+    q = np.zeros(1, np.float32)
+    d = np.zeros(1, np.float32)
+    k = np.zeros(1, np.int32)
+    rc = lib().or_crp_pair(_p(X, _fp), len(X), _p(Y, _fp), len(Y), m, tau, kappa, int(oti), gamma_open, gamma_ext,
+                           _p(q, _fp), _p(d, _fp), _p(k, _i32p), _p(C, _u8p), _p(tr, _fp), _p(tc, _fp))
+    assert rc == 0
+    return {"qmax": float(q[0]), "dmax": float(d[0]), "oti": int(k[0]), "crp": C, "thr_row": tr, "thr_col": tc}
+
+
+def crp_dist(X, Y, k=0, m=9, tau=1):
+    X = np.ascontiguousarray(X, np.float32)
+    Y = np.ascontiguousarray(Y, np.float32)
+    Mp, Np = stacked_len(len(X), m, tau), stacked_len(len(Y), m, tau)
+    D = np.zeros((Mp, Np), np.float32)
+    lib().or_crp_dist(_p(X, _fp), len(X), _p(Y, _fp), len(Y), int(k), m, tau, _p(D, _fp))
+    return D
+
+
+def crp_batch(feats, off, lens, pairs, m=9, tau=1, kappa=0.095, oti=True, gamma_open=0.5, gamma_ext=0.5,
+              dmax=True, nthreads=0):
+    feats = np.ascontiguousarray(feats, np.float32)
+    off = np.ascontiguousarray(off, np.int64)
+    lens = np.ascontiguousarray(lens, np.int32)
+    pairs = np.ascontiguousarray(pairs, np.int32)
+    P = len(pairs)
+    q = np.zeros(P, np.float32)
+    d = np.zeros(P, np.float32)
+    k = np.zeros(P, np.int32)
+    rc = lib().or_crp_batch(_p(feats, _fp), _p(off, _i64p), _p(lens, _i32p), _p(pairs, _i32p), P, m, tau, kappa,
+                            int(oti), gamma_open, gamma_ext, _p(q, _fp), _p(d, _fp) if dmax else None,
+                            _p(k, _i32p), int(nthreads))
+    if rc != 0:
+        raise ValueError("a track is too short for the stacking")
+    return q, (d if dmax else None), k
+
+
+def align(C, gamma_open=0.5, gamma_ext=0.5, which=0):
+    C = np.ascontiguousarray(C, np.uint8)
+    return float(lib().or_align(_p(C, _u8p), C.shape[0], C.shape[1], gamma_open, gamma_ext, which))
+
+
+def sw_constrained(B):
+    B = np.ascontiguousarray(B, np.uint8)
+    return float(lib().or_sw_constrained(_p(B, _u8p), B.shape[0], B.shape[1]))
+
+
+def simple_sim(A, B, sslen=10):
+    A = np.ascontiguousarray(A, np.float64)
+    B = np.ascontiguousarray(B, np.float64)
+    return float(lib().or_simple_sim(_p(A, _dp), A.shape[1], _p(B, _dp), B.shape[1], sslen))
+
+
+def profile(X):
+    X = np.ascontiguousarray(X, np.float32)
+    p = np.zeros(12, np.float32)
+    lib().or_track_profile(_p(X, _fp), len(X), _p(p, _fp))
+    return p
+
+
+def oti(pq, pr):
+    pq = np.ascontiguousarray(pq, np.float32)
+    pr = np.ascontiguousarray(pr, np.float32)
+    return int(lib().or_oti(_p(pq, _fp), _p(pr, _fp)))

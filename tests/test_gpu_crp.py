@@ -1,0 +1,68 @@
+"""GPU parity: Serra09/Chen CRP + Qmax/dmax (HIP, through the C-ABI) vs the CPU oracle.
+
+Bar (BASELINE.json north_star): OTI index and CRP mask bit-exact; Qmax/dmax exact (the DP
+values are multiples of 0.5 in f32); thresholds and distances bit-exact (same canonical
+rounding sequence, oracle/crp_oracle.cpp header).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from acoss import _lib, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(rng, M, N):
+    base = synthetic.base_sequence(rng, max(M, N))
+    X = synthetic.render(rng, base[:M])
+    Y = synthetic.render(rng, np.roll(synthetic.cover_of(rng, base, N), 0, 1))
+    return X, Y
+
+
+@pytest.mark.parametrize("M,N,m,tau,oti", [(60, 70, 9, 1, True), (300, 257, 9, 1, True), (523, 611, 9, 2, True),
+                                            (200, 180, 4, 1, False), (2000, 2000, 9, 1, True)])
+def test_crp_pair_intermediates_bitexact(M, N, m, tau, oti):
+    rng = np.random.Generator(np.random.PCG64(M * 1000 + N))
+    X, Y = _pair(rng, M, N)
+    ref = oracle.crp_pair(X, Y, m=m, tau=tau, kappa=0.095, oti=oti)
+    got = _lib.crp_pair(X, Y, _lib.crp_params(m=m, tau=tau, kappa=0.095, oti=oti))
+    assert int(got["oti"].item()) == ref["oti"]
+    Dref = oracle.crp_dist(X, Y, ref["oti"], m, tau)
+    np.testing.assert_array_equal(got["dist"].cpu().numpy().view(np.uint32), Dref.view(np.uint32))
+    np.testing.assert_array_equal(got["thr_row"].cpu().numpy().view(np.uint32), ref["thr_row"].view(np.uint32))
+    np.testing.assert_array_equal(got["thr_col"].cpu().numpy().view(np.uint32), ref["thr_col"].view(np.uint32))
+    np.testing.assert_array_equal(got["crp"].cpu().numpy(), ref["crp"])
+
+
+def test_crp_align_batch_matches_oracle():
+    tracks, labels = synthetic.make_corpus("covers80", frames=300, seed=7)
+    tracks = tracks[:24]
+    feats, off, lens = synthetic.pack(tracks)
+    pairs = np.array([(i, j) for i in range(24) for j in range(i + 1, 24)], np.int32)
+    q, d, k = oracle.crp_batch(feats, off, lens, pairs)
+    got = _lib.crp_align(feats, off, lens, int(lens.max()), pairs, _lib.crp_params(), qmax=True, dmax=True, oti=True)
+    np.testing.assert_array_equal(got["oti"].cpu().numpy(), k)
+    np.testing.assert_array_equal(got["qmax"].cpu().numpy(), q)
+    np.testing.assert_array_equal(got["dmax"].cpu().numpy(), d)
+
+
+@pytest.mark.parametrize("M,N,go,ge,align", [(5, 5, 0.5, 0.5, 0), (300, 200, 0.5, 0.5, 0), (300, 200, 0.5, 0.5, 1),
+                                             (2100, 90, 0.5, 0.5, 0), (2100, 90, 0.5, 0.5, 1),
+                                             (4200, 70, 0.7, 0.3, 0), (4200, 70, 0.7, 0.3, 1),
+                                             (257, 4100, 1.0, 0.5, 0)])
+def test_align_crp_matches_oracle(M, N, go, ge, align):
+    rng = np.random.Generator(np.random.PCG64(M + 7 * N))
+    C = (rng.random((M, N)) < 0.15).astype(np.uint8)
+    for t in range(min(M, N)):
+        C[t, t] = 1
+    ref = oracle.align(C, go, ge, align)
+    got = float(_lib.align_crp(C, align, go, ge).item())
+    assert got == ref
+
+
+def test_align_crp_rejects_nonbinary():
+    C = np.zeros((10, 10), np.uint8)
+    C[3, 4] = 2
+    with pytest.raises(_lib.AcossHipError):
+        _lib.align_crp(C)
