@@ -46,6 +46,8 @@ SIGNATURES = {
     "acoss_wcsm": [_vp, _i32, _i32, _i32, _i32, _f32, _vp, _vp],
     "acoss_simple_mp": [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _i32, _vp, _vp, _vp],
     "acoss_release_workspace": [],
+    "acoss_profile_enable": [ctypes.c_int],
+    "acoss_profile_read": [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int],
 }
 
 _lib = None
@@ -70,6 +72,8 @@ def load_library(path=None):
     lib.acoss_last_error.argtypes = []
     lib.acoss_version.restype = ctypes.c_char_p
     lib.acoss_version.argtypes = []
+    lib.acoss_profile_phase_name.restype = ctypes.c_char_p
+    lib.acoss_profile_phase_name.argtypes = [ctypes.c_int]
     if path is None:
         _lib = lib
     return lib
@@ -169,3 +173,19 @@ def align_crp(C, align=0, gamma_open=0.5, gamma_ext=0.5):
                              float(gamma_ext), _ptr(out), _stream())
     _check(rc, "acoss_align_crp")
     return out
+
+
+def profile_enable(on=True):
+    load_library().acoss_profile_enable(1 if on else 0)
+
+
+def profile_read():
+    """{phase name: (total_ms, launches)} for the phases recorded since profile_enable(True)."""
+    lib = load_library()
+    n = 32
+    ms = (ctypes.c_double * n)()
+    cnt = (ctypes.c_int64 * n)()
+    k = lib.acoss_profile_read(ms, cnt, n)
+    if k < 0:
+        _check(k, "acoss_profile_read")
+    return {lib.acoss_profile_phase_name(i).decode(): (ms[i], int(cnt[i])) for i in range(k) if cnt[i] > 0}

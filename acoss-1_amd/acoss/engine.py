@@ -1,0 +1,49 @@
+"""Device-resident song banks and the batched pair scorers built on the C-ABI.
+
+A bank packs every track of a corpus once into HBM (one contiguous (sum n, 12) float32
+block + offsets/lengths, SURVEY.md §8f row 3 layout); the scorers then take (P, 2) pair
+index lists and return one score per pair, computed by the HIP kernels in a single
+stream-ordered call. This replaces the reference's per-pair Python loop
+(CoverAlgorithm.similarity, acoss/algorithms/algorithm_template.py:121-140 and the plugin
+overrides) with one batched call per pair chunk.
+"""
+import numpy as np
+
+from . import _lib
+from .synthetic import pack
+
+
+def stacked_len(n, m=9, tau=1):
+    """essentia stackChromaFrames count (crp.hip stacked_len)."""
+    inc = m * tau
+    return 0 if n <= inc else (n - inc + tau - 1) // tau
+
+
+class ChromaBank:
+    """12-bin chroma of a whole corpus resident on the current GPU."""
+
+    def __init__(self, tracks):
+        torch = _lib._torch()
+        feats, off, lens = pack([np.asarray(t, np.float32) for t in tracks])
+        self.n_tracks = len(tracks)
+        self.lens = lens
+        self.max_len = int(lens.max()) if len(lens) else 0
+        self.feats = torch.as_tensor(feats).cuda()
+        self.off = torch.as_tensor(off).cuda()
+        self.len = torch.as_tensor(lens).cuda()
+
+    def crp_align(self, pairs, m=9, tau=1, kappa=0.095, oti=True, gamma_open=0.5, gamma_ext=0.5, qmax=True,
+                  dmax=False, want_oti=False):
+        """Serra09 (Qmax) / Chen (dmax) scores for (query, reference) pairs."""
+        torch = _lib._torch()
+        pairs = torch.as_tensor(np.asarray(pairs, np.int32)) if not isinstance(pairs, torch.Tensor) else pairs
+        if pairs.numel() == 0:
+            z = torch.zeros(0, dtype=torch.float32, device="cuda")
+            return {k: z for k, on in (("qmax", qmax), ("dmax", dmax), ("oti", want_oti)) if on}
+        short = [i for i in np.unique(pairs.cpu().numpy()) if stacked_len(self.lens[i], m, tau) <= 0]
+        if short:
+            raise ValueError("tracks %s are too short for frameStackSize=%d, frameStackStride=%d (essentia raises)"
+                             % (short[:5], m, tau))
+        params = _lib.crp_params(m, tau, kappa, oti, gamma_open, gamma_ext)
+        return _lib.crp_align(self.feats, self.off, self.len, self.max_len, pairs.cuda(), params, qmax=qmax,
+                              dmax=dmax, oti=want_oti)

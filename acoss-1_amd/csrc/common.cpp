@@ -6,6 +6,7 @@
 #include <map>
 #include <mutex>
 #include <utility>
+#include <vector>
 
 namespace acoss {
 
@@ -23,11 +24,11 @@ void clear_error() { g_err[0] = '\0'; }
 const char* last_error() { return g_err; }
 
 namespace {
+std::mutex g_mu;
 struct Buf {
   void* ptr = nullptr;
   size_t bytes = 0;
 };
-std::mutex g_mu;
 std::map<std::pair<int, int>, Buf> g_ws;  // (device, slot) -> buffer
 }  // namespace
 
@@ -68,7 +69,85 @@ int release_all_workspaces() {
   return ACOSS_OK;
 }
 
+namespace {
+struct PhaseRec {
+  int phase;
+  hipEvent_t a, b;
+};
+bool g_prof = false;
+std::vector<PhaseRec> g_recs;
+std::vector<hipEvent_t> g_pool;
+PhaseRec g_open[PH_COUNT];
+const char* kPhaseNames[PH_COUNT] = {"prep",      "oti",     "select_rows", "select_cols", "crp_mask", "dp_qmax",
+                                     "dp_dmax",   "sw",      "csm",         "binarize",    "wcsm",     "simple_mp"};
+hipEvent_t get_event() {
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+}  // namespace
+
+bool profiling() { return g_prof; }
+
+void prof_begin(int phase, hipStream_t s) {
+  if (!g_prof) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_open[phase].phase = phase;
+  g_open[phase].a = get_event();
+  (void)hipEventRecord(g_open[phase].a, s);
+}
+
+void prof_end(int phase, hipStream_t s) {
+  if (!g_prof) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  PhaseRec r = g_open[phase];
+  r.b = get_event();
+  (void)hipEventRecord(r.b, s);
+  g_recs.push_back(r);
+}
+
 }  // namespace acoss
+
+using namespace acoss;
+
+// Enable (1) / disable (0) phase timing; enabling clears what was recorded.
+extern "C" int acoss_profile_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_prof = on != 0;
+  for (auto& r : g_recs) {
+    g_pool.push_back(r.a);
+    g_pool.push_back(r.b);
+  }
+  g_recs.clear();
+  return ACOSS_OK;
+}
+
+// Synchronises the recorded events and writes, per phase, the total milliseconds and the
+// number of launches recorded. Returns the number of phases (PH_COUNT).
+extern "C" int acoss_profile_read(double* total_ms, int64_t* count, int n) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (int i = 0; i < n && i < PH_COUNT; ++i) {
+    total_ms[i] = 0.0;
+    count[i] = 0;
+  }
+  for (auto& r : g_recs) {
+    if (hipEventSynchronize(r.b) != hipSuccess) return ACOSS_E_HIP;
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) return ACOSS_E_HIP;
+    if (r.phase < n) {
+      total_ms[r.phase] += ms;
+      count[r.phase] += 1;
+    }
+  }
+  return PH_COUNT;
+}
+
+extern "C" const char* acoss_profile_phase_name(int i) { return (i >= 0 && i < PH_COUNT) ? kPhaseNames[i] : ""; }
 
 extern "C" const char* acoss_last_error(void) { return acoss::last_error(); }
 extern "C" int acoss_release_workspace(void) { return acoss::release_all_workspaces(); }

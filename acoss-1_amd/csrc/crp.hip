@@ -724,7 +724,9 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   if ((rc = prepare_stage(m, ld, &st))) return rc;
   float *prof, *NX;
   int ldn;
+  prof_begin(PH_PREP, s);
   if ((rc = run_prep(feats, track_off, track_len, n_tracks, max_len, m, tau, s, &prof, &NX, &ldn))) return rc;
+  prof_end(PH_PREP, s);
 
   // per-pair slot: oti, dims, thr/T rows+cols, maskT, band boundary
   const int nstrips = (L + 31) / 32;
@@ -761,28 +763,40 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   for (int64_t base = 0; base < n_pairs; base += nb_alloc) {
     const int nb = (int)((n_pairs - base) < nb_alloc ? (n_pairs - base) : nb_alloc);
     const int32_t* pb = pairs + 2 * base;
+    prof_begin(PH_OTI, s);
     hipLaunchKernelGGL(k_pair_oti, dim3((nb + 255) / 256), dim3(256), 0, s, prof, track_len, pb, (int64_t)nb,
                        params->oti, m, tau, w_oti, w_dims);
     ACOSS_LAUNCH_CHECK();
+    prof_end(PH_OTI, s);
     CrpBatch B{feats, track_off, track_len, NX, ldn, pb, w_oti, w_dims, m, tau};
+    prof_begin(PH_SEL_ROWS, s);
     hipLaunchKernelGGL(k_crp_select<false>, dim3((L + st.R - 1) / st.R, nb), dim3(256), st.sel_lds, s, B, st.R, ld,
                        params->kappa, w_thr_r, w_T_r, thr_stride);
     ACOSS_LAUNCH_CHECK();
+    prof_end(PH_SEL_ROWS, s);
+    prof_begin(PH_SEL_COLS, s);
     hipLaunchKernelGGL(k_crp_select<true>, dim3((L + st.R - 1) / st.R, nb), dim3(256), st.sel_lds, s, B, st.R, ld,
                        params->kappa, w_thr_c, w_T_c, thr_stride);
     ACOSS_LAUNCH_CHECK();
+    prof_end(PH_SEL_COLS, s);
+    prof_begin(PH_MASK, s);
     hipLaunchKernelGGL(k_crp_panel<0>, dim3((L + kPanelW - 1) / kPanelW, nstrips, nb), dim3(256), st.pan_lds, s, B,
                        w_T_r, w_T_c, thr_stride, w_mask, mask_stride, ld, (float*)nullptr);
     ACOSS_LAUNCH_CHECK();
+    prof_end(PH_MASK, s);
     if (qmax_out) {
+      prof_begin(PH_DP_QMAX, s);
       launch_dp<0>(eqg, nb, w_mask, mask_stride, ld, w_dims, params->gamma_open, params->gamma_ext, w_bnd,
                    bnd_stride, qmax_out + base, s);
       ACOSS_LAUNCH_CHECK();
+      prof_end(PH_DP_QMAX, s);
     }
     if (dmax_out) {
+      prof_begin(PH_DP_DMAX, s);
       launch_dp<1>(eqg, nb, w_mask, mask_stride, ld, w_dims, params->gamma_open, params->gamma_ext, w_bnd,
                    bnd_stride, dmax_out + base, s);
       ACOSS_LAUNCH_CHECK();
+      prof_end(PH_DP_DMAX, s);
     }
     if (oti_out) ACOSS_HIP_CHECK(hipMemcpyAsync(oti_out + base, w_oti, 4 * nb, hipMemcpyDeviceToDevice, s));
   }

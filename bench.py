@@ -1,0 +1,218 @@
+#!/usr/bin/env python
+"""bench.py — song-pairs/s of the Serra09 hot path (OTI -> CRP -> Qmax) on MI355X.
+
+Metric (BASELINE.json): "song-pairs/sec (CSM+Qmax) on 12-d HPCP, ~2000 frames/track; MAP parity".
+Workload (configs[1]): covers80-shaped corpus (164 tracks: 77x2, 2x3, 1x4 cliques), synthetic
+12-d HPCP, every track exactly 2000 frames at the CSM input (M = N = 2000, M' = N' = 1991),
+essentia defaults m=9, tau=1, kappa=0.095, OTI on, gamma 0.5/0.5. A step = every unordered
+pair (i < j) of the corpus scored once = 13,366 pairs at N=1. Features are resident in HBM
+before the timed region.
+
+Multi-GPU (one process per GPU, torchrun): weak scaling. The corpus grows to
+round(164 * sqrt(N)) tracks (the covers80 clique pattern repeated), so each rank scores a
+cost-balanced row stripe of ~13.4k pairs; each step ends with ONE all-gather of the stripes
+(RCCL over xGMI) that assembles the full N x N score matrix on every rank. value = all
+pairs of all ranks / max-over-ranks time.
+
+Also reported: roofline of the path (SURVEY.md §8d ops_pair) with per-kernel HIP-event
+times, MAP/MR1 of the assembled matrix (reference normalisation + evaluation), and the CPU
+baseline: the oracle (C++ restatement, oracle/) timed on the host cores of this node over a
+bounded random sample of the same pairs, whose Qmax values are also checked for equality.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "acoss-1_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+PEAK_F32_TFLOPS = 157.3  # MI355X fp32 (matrix = vector) dense peak, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def ops_pair(M, N, m=9, tau=1):
+    """2*12*M*N (Gram) + 32*M'*N' (window, norms, sqrt, thresholds, DP)."""
+    Mp = max(0, -(-(M - m * tau) // tau))
+    Np = max(0, -(-(N - m * tau) // tau))
+    return 2.0 * 12 * M * N + 32.0 * Mp * Np
+
+
+def corpus_tracks(n_gpus, frames, seed):
+    from acoss import synthetic
+    sizes = synthetic.clique_sizes("covers80")
+    target = int(round(164 * math.sqrt(n_gpus)))
+    pattern = []
+    while sum(pattern) < target:
+        pattern.extend(sizes)
+    # trim the pattern to exactly `target` tracks
+    out, tot = [], 0
+    for s in pattern:
+        if tot >= target:
+            break
+        s = min(s, target - tot)
+        out.append(s)
+        tot += s
+    rng = np.random.Generator(np.random.PCG64(seed))
+    tracks, labels = [], []
+    for lab, size in enumerate(out):
+        base = synthetic.base_sequence(rng, frames)
+        for v in range(size):
+            seq = base if v == 0 else synthetic.cover_of(rng, base, frames)
+            tracks.append(synthetic.render(rng, seq))
+            labels.append(lab)
+    return tracks, np.asarray(labels, np.int32)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=2000)
+    ap.add_argument("--seed", type=int, default=20250101)
+    ap.add_argument("--cpu-sample", type=int, default=192, help="pairs timed on the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from acoss import _lib, distributed, evaluation
+    from acoss.engine import ChromaBank
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    n_gpus = world
+
+    tracks, labels = corpus_tracks(n_gpus, args.frames, args.seed)
+    T = len(tracks)
+    lens = np.array([len(t) for t in tracks], np.int32)
+    bank = ChromaBank(tracks)
+    bounds = distributed.stripe_bounds(lens, world, symmetric=True)
+    r0, r1 = bounds[rank]
+    my_pairs_np = distributed.stripe_pairs(T, r0, r1, symmetric=True)
+    my_pairs = torch.as_tensor(my_pairs_np).cuda()
+    total_pairs = T * (T - 1) // 2
+
+    def step():
+        out = bank.crp_align(my_pairs, qmax=True)
+        blk = distributed.scatter_stripe(my_pairs, out["qmax"], r0, r1, T)
+        if world > 1:
+            return distributed.all_gather_stripes(blk, bounds)
+        return blk
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        D = step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        D = step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt / args.steps * 1e3
+    value = total_pairs * args.steps / dt
+
+    # ---- per-kernel HIP-event times of one profiled step (same stream, same launches) ----
+    phases = {}
+    if not args.no_profile:
+        _lib.profile_enable(True)
+        bank.crp_align(my_pairs, qmax=True)
+        torch.cuda.synchronize()
+        phases = _lib.profile_read()
+        _lib.profile_enable(False)
+
+    # ---- MAP / MR1 on the assembled matrix (reference normalisation + evaluation) ----
+    Dfull = D.cpu().numpy()                                       # (T, T) upper triangle filled
+    Dsym = (Dfull + Dfull.T).astype(np.float32)                    # all_pairwise: Ds += Ds.T (:188-191)
+    Dsym = Dsym / np.sqrt(lens.astype(np.float32))[None, :]       # Serra09.normalize_by_length (:71-83)
+    MR, MRR, MDR, MAP, tops = evaluation.eval_statistics(Dsym, labels)
+
+    result = None
+    if rank == 0:
+        M = N = args.frames
+        opp = ops_pair(M, N)
+        launch_ms = sum(v[0] for v in phases.values()) if phases else ms_per_step
+        batch_pairs = len(my_pairs_np)
+        kernels = {k: {"ms_per_launch": v[0] / max(1, v[1]), "launches": v[1]} for k, v in phases.items()}
+        dom = max(kernels.items(), key=lambda kv: kv[1]["ms_per_launch"] * kv[1]["launches"])[0] if kernels else None
+        achieved = opp * batch_pairs / (launch_ms * 1e-3) / 1e12
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "traffic_latest.json")
+        if os.path.exists(tfile):
+            try:
+                traffic = json.load(open(tfile)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": traffic,
+                    "kernel": "acoss_crp_align (one call = oti+select_rows+select_cols+crp_mask+dp_qmax on %d pairs)"
+                              % batch_pairs,
+                    "ops_per_pair": opp, "launch_ms": round(launch_ms, 3), "dominant_kernel": dom,
+                    "kernels": kernels}
+
+        cpu = None
+        if args.cpu_sample > 0:
+            import oracle
+            rng = np.random.Generator(np.random.PCG64(1234))
+            sel = rng.choice(len(my_pairs_np), size=min(args.cpu_sample, len(my_pairs_np)), replace=False)
+            sp = my_pairs_np[sel]
+            from acoss.synthetic import pack
+            feats, off, ln = pack(tracks)
+            nth = args.cpu_threads or min(16, os.cpu_count() or 1)
+            t0 = time.perf_counter()
+            q, _, _ = oracle.crp_batch(feats, off, ln, sp, dmax=False, nthreads=nth)
+            cdt = time.perf_counter() - t0
+            gq = Dfull[sp[:, 0], sp[:, 1]]
+            parity = bool(np.array_equal(gq.astype(np.float32), q))
+            cpu = {"value": round(len(sp) / cdt, 3), "unit": "song-pairs/s", "cores": nth, "kind": "port",
+                   "sample": "%d random pairs of the same corpus (2000x2000 frames), oracle/crp_oracle.cpp, "
+                             "%d OpenMP threads, %.1f s" % (len(sp), nth, cdt),
+                   "qmax_bitexact_vs_gpu": parity}
+
+        result = {
+            "metric": "song-pairs/sec (CSM+Qmax) on 12-d HPCP, ~2000 frames/track; MAP parity",
+            "value": round(value, 2), "unit": "song-pairs/s", "n_gpus": n_gpus, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "covers80-shaped synthetic HPCP, Serra09 CRP+Qmax, all unordered pairs",
+                       "tracks": T, "pairs_per_step": total_pairs, "frames_per_track": args.frames,
+                       "m": 9, "tau": 1, "kappa": 0.095, "oti": True, "parallelism": "pair-matrix row stripes dp%d"
+                       % n_gpus},
+            "map": round(float(MAP), 6), "mr1": round(float(MR), 4), "mrr": round(float(MRR), 6),
+            "top1": int(tops[0]),
+            "roofline": roofline, "cpu_baseline": cpu,
+            "speedup_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
+        }
+        print(json.dumps(result))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -47,6 +47,14 @@ const char* acoss_version(void);
 const char* acoss_last_error(void);
 int acoss_release_workspace(void);
 
+/* Optional phase timing (bench.py): HIP events recorded around every kernel launch on the
+ * launch stream. enable(1) clears and starts recording, enable(0) stops. read() synchronises
+ * the events and fills total_ms[i] / count[i] for phase i < n; returns the phase count.
+ * Phase names: acoss_profile_phase_name(i). */
+int acoss_profile_enable(int on);
+int acoss_profile_read(double* total_ms, int64_t* count, int n);
+const char* acoss_profile_phase_name(int i);
+
 /* ---------------------------------------------------------------------------------
  * Serra09 / LateFusionChen hot path for a batch of song pairs (A1/A4/A9/A10/A16).
  * Replaces, per pair (i, j) = (pairs[2p], pairs[2p+1]):
