@@ -54,10 +54,53 @@ __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a -
 // ---- device helpers ----
 constexpr int kWave = 64;
 
-__device__ inline float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
+// ---- wave64 collectives on DPP (VALU, no LDS round trip) ----
+// update_dpp(old, src, ctrl, row_mask, bank_mask, bound_ctrl): row_shr:n = 0x110+n,
+// row_bcast:15 = 0x142, row_bcast:31 = 0x143 (GFX9 family, gfx950 included).
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ unsigned dpp_u32(unsigned old, unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWMASK, 0xf, false);
+}
+
+// Inclusive scan (sum) over the 64 lanes.
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  unsigned v = (unsigned)x;
+  v += dpp_u32<0x111>(0u, v);
+  v += dpp_u32<0x112>(0u, v);
+  v += dpp_u32<0x114>(0u, v);
+  v += dpp_u32<0x118>(0u, v);
+  v += dpp_u32<0x142, 0xa>(0u, v);
+  v += dpp_u32<0x143, 0xc>(0u, v);
+  return (int)v;
+}
+
+// Reductions: the scan pattern leaves the total in lane 63; readlane broadcasts it (SGPR).
+__device__ __forceinline__ int wave_sum(int x) { return __builtin_amdgcn_readlane(wave_incl_scan(x), 63); }
+
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+  const unsigned I = 0xffffffffu;
+  v = min(v, dpp_u32<0x111>(I, v));
+  v = min(v, dpp_u32<0x112>(I, v));
+  v = min(v, dpp_u32<0x114>(I, v));
+  v = min(v, dpp_u32<0x118>(I, v));
+  v = min(v, dpp_u32<0x142, 0xa>(I, v));
+  v = min(v, dpp_u32<0x143, 0xc>(I, v));
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+  v = max(v, dpp_u32<0x111>(0u, v));
+  v = max(v, dpp_u32<0x112>(0u, v));
+  v = max(v, dpp_u32<0x114>(0u, v));
+  v = max(v, dpp_u32<0x118>(0u, v));
+  v = max(v, dpp_u32<0x142, 0xa>(0u, v));
+  v = max(v, dpp_u32<0x143, 0xc>(0u, v));
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Max of non-negative floats / doubles: order-preserving on the bit patterns.
+__device__ __forceinline__ float wave_max(float v) {
+  return __builtin_bit_cast(float, wave_max_u32(__builtin_bit_cast(unsigned, v)));
 }
 
 __device__ inline double wave_max(double v) {
@@ -66,28 +109,8 @@ __device__ inline double wave_max(double v) {
   return v;
 }
 
-__device__ inline int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-
-__device__ inline unsigned wave_min_u32(unsigned v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o));
-  return v;
-}
-
-// Inclusive scan over the 64 lanes of a wave.
-__device__ inline int wave_incl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(v, o);
-    if (lane >= o) v += u;
-  }
-  return v;
-}
+// Value of lane `src` (wave-uniform) in every lane: v_readlane, no LDS.
+__device__ __forceinline__ int lane_bcast(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
 
 // Correctly rounded sqrt (hipcc default: -fhip-fp32-correctly-rounded-divide-sqrt).
 __device__ inline float sqrt_rn(float x) { return __builtin_sqrtf(x); }

@@ -23,7 +23,7 @@
 //    pass down one lane per step with __shfl_up; bands chain through a small HBM buffer.
 #include <cstdlib>
 
-#include "common.hpp"
+#include "crp_internal.hpp"
 
 namespace acoss {
 
@@ -99,6 +99,21 @@ __global__ void k_pair_oti(const float* __restrict__ prof, const int32_t* __rest
   }
   oti[p] = best;
   dims[p] = make_int2(stacked_len(len[a], m, tau), stacked_len(len[b], m, tau));
+}
+
+// yrot[p][f][c] = reference[f][(c - oti[p]) mod 12]  (np.roll of every reference frame).
+__global__ void k_rotate_ref(const float* __restrict__ feats, const int64_t* __restrict__ off,
+                             const int32_t* __restrict__ len, const int32_t* __restrict__ pairs,
+                             const int32_t* __restrict__ oti, float* __restrict__ yrot, int64_t stride) {
+  const int p = blockIdx.y;
+  const int b = pairs[2 * p + 1];
+  const int n = len[b], k = oti[p];
+  const float* src = feats + off[b] * 12;
+  float* dst = yrot + (size_t)p * stride;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n * 12; e += gridDim.x * blockDim.x) {
+    const int f = e / 12, c = e - f * 12;
+    dst[e] = src[(size_t)f * 12 + (c - k + 12) % 12];
+  }
 }
 
 // --------------------------------------------------------------------------------------
@@ -294,17 +309,6 @@ __device__ inline void block_percentile(const unsigned* keys, int n, float kappa
 // (TRANS=false: rows of the CRP / query frames) or columns (TRANS=true: reference frames).
 // Dynamic LDS: Dst[R][ld] keys | panel buffers. Hist aliases the Ys|Gs panel region.
 // --------------------------------------------------------------------------------------
-struct CrpBatch {
-  const float* feats;
-  const int64_t* off;
-  const int32_t* len;
-  const float* NX;  // stacked norms, track t at NX[t*ldn]
-  int ldn;
-  const int32_t* pairs;
-  const int32_t* oti;
-  const int2* dims;
-  int m, tau;
-};
 
 template <bool TRANS>
 __global__ __launch_bounds__(256) void k_crp_select(CrpBatch B, int R, int ld, float kappa, float* __restrict__ thr,
@@ -671,6 +675,39 @@ void launch_dp(bool eqg, int nb, const uint32_t* maskT, int64_t mstride, int ld,
                        bstride, out);
 }
 
+// Thresholds of one side: fast m=9 path (crp_select.hip) unless ACOSS_SELECT_GENERIC is set
+// or the shape is outside it; otherwise the generic LDS-Gram kernel above.
+int run_select(bool trans, const Stage& st, const CrpBatch& B, int nb, int L, int ld, float kappa, float* thr, float* T,
+               int64_t thr_stride, hipStream_t s) {
+  static const bool generic = getenv("ACOSS_SELECT_GENERIC") != nullptr;
+  if (!generic) {
+    const int rc = launch_select16(trans, B, nb, L, kappa, thr, T, thr_stride, s);
+    if (rc != 1) return rc;
+  }
+  if (trans)
+    hipLaunchKernelGGL(k_crp_select<true>, dim3((L + st.R - 1) / st.R, nb), dim3(256), st.sel_lds, s, B, st.R, ld,
+                       kappa, thr, T, thr_stride);
+  else
+    hipLaunchKernelGGL(k_crp_select<false>, dim3((L + st.R - 1) / st.R, nb), dim3(256), st.sel_lds, s, B, st.R, ld,
+                       kappa, thr, T, thr_stride);
+  ACOSS_LAUNCH_CHECK();
+  return ACOSS_OK;
+}
+
+// CRP words: fast m=9 kernel (crp_mask.hip) unless ACOSS_MASK_GENERIC is set.
+int run_mask(const Stage& st, const CrpBatch& B, int nb, int L, int nstrips, const float* Tr, const float* Tc,
+             int64_t thr_stride, uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s) {
+  static const bool generic = getenv("ACOSS_MASK_GENERIC") != nullptr;
+  if (!generic) {
+    const int rc = launch_mask9(B, nb, L, Tr, Tc, thr_stride, maskT, mask_stride, ld, s);
+    if (rc != 1) return rc;
+  }
+  hipLaunchKernelGGL(k_crp_panel<0>, dim3((L + kPanelW - 1) / kPanelW, nstrips, nb), dim3(256), st.pan_lds, s, B,
+                     Tr, Tc, thr_stride, maskT, mask_stride, ld, (float*)nullptr);
+  ACOSS_LAUNCH_CHECK();
+  return ACOSS_OK;
+}
+
 // Per-track prep into workspace slot 0: prof (n_tracks x 12) | NX (n_tracks x ldn).
 int run_prep(const float* feats, const int64_t* off, const int32_t* len, int n_tracks, int max_len, int m, int tau,
              hipStream_t s, float** prof, float** NX, int* ldn) {
@@ -734,7 +771,9 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   const int64_t thr_stride = ld;
   const int64_t mask_stride = (int64_t)nstrips * ld;
   const int64_t bnd_stride = (int64_t)nbands * ld;
-  const size_t slot = 4 + 8 + 4 * (size_t)thr_stride * 4 + 4 * (size_t)mask_stride + 16 * (size_t)bnd_stride;
+  const int64_t yrot_stride = (int64_t)align_up((size_t)max_len * 12, 64);
+  const size_t slot = 4 + 8 + 4 * (size_t)thr_stride * 4 + 4 * (size_t)mask_stride + 16 * (size_t)bnd_stride +
+                      4 * (size_t)yrot_stride;
   size_t budget = (size_t)2 << 30;
   if (const char* e = getenv("ACOSS_WS_BYTES")) budget = strtoull(e, nullptr, 10);
   int64_t nbmax = (int64_t)(budget / slot);
@@ -758,6 +797,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   float* w_T_c = reinterpret_cast<float*>(carve(4 * thr_stride * nb_alloc));
   uint32_t* w_mask = reinterpret_cast<uint32_t*>(carve(4 * mask_stride * nb_alloc));
   float4* w_bnd = reinterpret_cast<float4*>(carve(16 * bnd_stride * nb_alloc));
+  float* w_yrot = reinterpret_cast<float*>(carve(4 * yrot_stride * nb_alloc));
 
   const bool eqg = params->gamma_open == params->gamma_ext;
   for (int64_t base = 0; base < n_pairs; base += nb_alloc) {
@@ -767,22 +807,19 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
     hipLaunchKernelGGL(k_pair_oti, dim3((nb + 255) / 256), dim3(256), 0, s, prof, track_len, pb, (int64_t)nb,
                        params->oti, m, tau, w_oti, w_dims);
     ACOSS_LAUNCH_CHECK();
-    prof_end(PH_OTI, s);
-    CrpBatch B{feats, track_off, track_len, NX, ldn, pb, w_oti, w_dims, m, tau};
-    prof_begin(PH_SEL_ROWS, s);
-    hipLaunchKernelGGL(k_crp_select<false>, dim3((L + st.R - 1) / st.R, nb), dim3(256), st.sel_lds, s, B, st.R, ld,
-                       params->kappa, w_thr_r, w_T_r, thr_stride);
+    hipLaunchKernelGGL(k_rotate_ref, dim3(16, nb), dim3(256), 0, s, feats, track_off, track_len, pb, w_oti, w_yrot,
+                       yrot_stride);
     ACOSS_LAUNCH_CHECK();
+    prof_end(PH_OTI, s);
+    CrpBatch B{feats, track_off, track_len, NX, ldn, pb, w_oti, w_dims, m, tau, w_yrot, yrot_stride};
+    prof_begin(PH_SEL_ROWS, s);
+    if ((rc = run_select(false, st, B, nb, L, ld, params->kappa, w_thr_r, w_T_r, thr_stride, s))) return rc;
     prof_end(PH_SEL_ROWS, s);
     prof_begin(PH_SEL_COLS, s);
-    hipLaunchKernelGGL(k_crp_select<true>, dim3((L + st.R - 1) / st.R, nb), dim3(256), st.sel_lds, s, B, st.R, ld,
-                       params->kappa, w_thr_c, w_T_c, thr_stride);
-    ACOSS_LAUNCH_CHECK();
+    if ((rc = run_select(true, st, B, nb, L, ld, params->kappa, w_thr_c, w_T_c, thr_stride, s))) return rc;
     prof_end(PH_SEL_COLS, s);
     prof_begin(PH_MASK, s);
-    hipLaunchKernelGGL(k_crp_panel<0>, dim3((L + kPanelW - 1) / kPanelW, nstrips, nb), dim3(256), st.pan_lds, s, B,
-                       w_T_r, w_T_c, thr_stride, w_mask, mask_stride, ld, (float*)nullptr);
-    ACOSS_LAUNCH_CHECK();
+    if ((rc = run_mask(st, B, nb, L, nstrips, w_T_r, w_T_c, thr_stride, w_mask, mask_stride, ld, s))) return rc;
     prof_end(PH_MASK, s);
     if (qmax_out) {
       prof_begin(PH_DP_QMAX, s);
@@ -823,7 +860,8 @@ extern "C" int acoss_crp_pair(const float* X, int32_t M, const float* Y, int32_t
   // packed features + tables in workspace slot 2
   const int nstrips = (Mp + 31) / 32;
   const size_t fbytes = align_up((size_t)(M + N) * 12 * 4, 256);
-  const size_t bytes = fbytes + 256 * 4 + 4 * 4 * (size_t)ld + 4 * (size_t)nstrips * ld;
+  const size_t ybytes = align_up((size_t)N * 12 * 4, 256);
+  const size_t bytes = fbytes + 256 * 4 + 4 * 4 * (size_t)ld + 4 * (size_t)nstrips * ld + ybytes;
   char* ws = static_cast<char*>(workspace(2, bytes));
   if (!ws) return ACOSS_E_HIP;
   float* f = reinterpret_cast<float*>(ws);
@@ -838,6 +876,8 @@ extern "C" int acoss_crp_pair(const float* X, int32_t M, const float* Y, int32_t
   float* thr_c = T_r + ld;
   float* T_c = thr_c + ld;
   uint32_t* maskT = reinterpret_cast<uint32_t*>(T_c + ld);
+  float* yrot = reinterpret_cast<float*>(reinterpret_cast<char*>(maskT) + 4 * (size_t)nstrips * ld);
+  yrot = reinterpret_cast<float*>(align_up(reinterpret_cast<uintptr_t>(yrot), 256));
   const int64_t h_off[2] = {0, M};
   const int32_t h_len[2] = {M, N};
   const int32_t h_pairs[2] = {0, 1};
@@ -853,22 +893,18 @@ extern "C" int acoss_crp_pair(const float* X, int32_t M, const float* Y, int32_t
   hipLaunchKernelGGL(k_pair_oti, dim3(1), dim3(64), 0, s, prof, d_len, d_pairs, (int64_t)1, params->oti, m, tau,
                      d_oti, d_dims);
   ACOSS_LAUNCH_CHECK();
-  CrpBatch B{f, d_off, d_len, NX, ldn, d_pairs, d_oti, d_dims, m, tau};
-  hipLaunchKernelGGL(k_crp_select<false>, dim3((Mp + st.R - 1) / st.R, 1), dim3(256), st.sel_lds, s, B, st.R, ld,
-                     params->kappa, thr_r, T_r, (int64_t)ld);
+  hipLaunchKernelGGL(k_rotate_ref, dim3(16, 1), dim3(256), 0, s, f, d_off, d_len, d_pairs, d_oti, yrot, (int64_t)0);
   ACOSS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_crp_select<true>, dim3((Np + st.R - 1) / st.R, 1), dim3(256), st.sel_lds, s, B, st.R, ld,
-                     params->kappa, thr_c, T_c, (int64_t)ld);
-  ACOSS_LAUNCH_CHECK();
+  CrpBatch B{f, d_off, d_len, NX, ldn, d_pairs, d_oti, d_dims, m, tau, yrot, 0};
+  if ((rc = run_select(false, st, B, 1, L, ld, params->kappa, thr_r, T_r, (int64_t)ld, s))) return rc;
+  if ((rc = run_select(true, st, B, 1, L, ld, params->kappa, thr_c, T_c, (int64_t)ld, s))) return rc;
   if (dist) {
     hipLaunchKernelGGL(k_crp_panel<1>, dim3((Np + kPanelW - 1) / kPanelW, nstrips, 1), dim3(256), st.pan_lds, s, B,
                        T_r, T_c, (int64_t)ld, maskT, (int64_t)0, ld, dist);
     ACOSS_LAUNCH_CHECK();
   }
   if (crp) {
-    hipLaunchKernelGGL(k_crp_panel<0>, dim3((Np + kPanelW - 1) / kPanelW, nstrips, 1), dim3(256), st.pan_lds, s, B,
-                       T_r, T_c, (int64_t)ld, maskT, (int64_t)0, ld, (float*)nullptr);
-    ACOSS_LAUNCH_CHECK();
+    if ((rc = run_mask(st, B, 1, L, nstrips, T_r, T_c, (int64_t)ld, maskT, (int64_t)0, ld, s))) return rc;
     hipLaunchKernelGGL(k_unpack_mask, dim3((Np + 255) / 256, Mp), dim3(256), 0, s, maskT, ld, Mp, Np, crp);
     ACOSS_LAUNCH_CHECK();
   }
