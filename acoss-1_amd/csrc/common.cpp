@@ -79,7 +79,8 @@ std::vector<PhaseRec> g_recs;
 std::vector<hipEvent_t> g_pool;
 PhaseRec g_open[PH_COUNT];
 const char* kPhaseNames[PH_COUNT] = {"prep",      "oti",     "select_rows", "select_cols", "crp_mask", "dp_qmax",
-                                     "dp_dmax",   "sw",      "csm",         "binarize",    "wcsm",     "simple_mp"};
+                                     "dp_dmax",   "sw",      "csm",         "binarize",    "wcsm",     "simple_mp",
+                                     "sweep"};
 hipEvent_t get_event() {
   if (!g_pool.empty()) {
     hipEvent_t e = g_pool.back();

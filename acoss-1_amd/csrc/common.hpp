@@ -20,7 +20,7 @@ int release_all_workspaces();
 // Optional per-phase timing with HIP events recorded on the launch stream (bench.py reads it
 // through acoss_profile_read). Phases are small integers; names in common.cpp.
 enum Phase { PH_PREP = 0, PH_OTI, PH_SEL_ROWS, PH_SEL_COLS, PH_MASK, PH_DP_QMAX, PH_DP_DMAX, PH_SW, PH_CSM,
-             PH_BIN, PH_WCSM, PH_SIMPLE, PH_COUNT };
+             PH_BIN, PH_WCSM, PH_SIMPLE, PH_SWEEP, PH_COUNT };
 bool profiling();
 void prof_begin(int phase, hipStream_t s);
 void prof_end(int phase, hipStream_t s);

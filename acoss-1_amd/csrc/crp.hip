@@ -22,6 +22,7 @@
 //    columns skewed by one column per lane (anti-diagonal wavefront); the two boundary rows
 //    pass down one lane per step with __shfl_up; bands chain through a small HBM buffer.
 #include <cstdlib>
+#include <cstring>
 
 #include "crp_internal.hpp"
 
@@ -772,6 +773,15 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   const int64_t mask_stride = (int64_t)nstrips * ld;
   const int64_t bnd_stride = (int64_t)nbands * ld;
   const int64_t yrot_stride = (int64_t)align_up((size_t)max_len * 12, 64);
+  // split path (one sweep + two line-select kernels, crp_split.hip) needs 16-bit key planes
+  static const char* path_env = getenv("ACOSS_CRP_PATH");
+  const bool split = m == 9 && L <= 2048 && !(path_env && strcmp(path_env, "fused") == 0);
+  const int ldk = (int)align_up((size_t)L, 64);
+  const int64_t kstride = split ? (int64_t)L * ldk : 0;
+  // Two-level batching: a DP batch of nb_alloc pairs keeps its CRP words (0.5 MB per pair at
+  // 2000 frames) so the one-wave-per-pair DP launch is wide enough; the CRP itself runs in
+  // sub-batches whose 16-bit key planes (split path, 16 MB per pair) stay near the 256 MB
+  // Infinity Cache.
   const size_t slot = 4 + 8 + 4 * (size_t)thr_stride * 4 + 4 * (size_t)mask_stride + 16 * (size_t)bnd_stride +
                       4 * (size_t)yrot_stride;
   size_t budget = (size_t)2 << 30;
@@ -781,7 +791,15 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   if (nbmax < 1) nbmax = 1;
   if (nbmax > 65535) nbmax = 65535;
   const int64_t nb_alloc = n_pairs < nbmax ? n_pairs : nbmax;
-  char* ws = static_cast<char*>(workspace(1, slot * nb_alloc + 4096));
+  int64_t sub = nb_alloc;
+  if (split) {
+    size_t kbudget = (size_t)2 << 30;  // ~65 pairs at 2000 frames: enough blocks to fill 256 CUs
+    if (const char* e = getenv("ACOSS_KEY_BYTES")) kbudget = strtoull(e, nullptr, 10);
+    sub = (int64_t)(kbudget / (8 * (size_t)kstride));
+    if (sub < 1) sub = 1;
+    if (sub > nb_alloc) sub = nb_alloc;
+  }
+  char* ws = static_cast<char*>(workspace(1, slot * nb_alloc + 8 * (size_t)kstride * sub + 8192));
   if (!ws) return ACOSS_E_HIP;
   size_t o = 0;
   auto carve = [&](size_t bytes) {
@@ -798,6 +816,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   uint32_t* w_mask = reinterpret_cast<uint32_t*>(carve(4 * mask_stride * nb_alloc));
   float4* w_bnd = reinterpret_cast<float4*>(carve(16 * bnd_stride * nb_alloc));
   float* w_yrot = reinterpret_cast<float*>(carve(4 * yrot_stride * nb_alloc));
+  uint16_t* w_kpl = reinterpret_cast<uint16_t*>(carve(8 * kstride * sub));
 
   const bool eqg = params->gamma_open == params->gamma_ext;
   for (int64_t base = 0; base < n_pairs; base += nb_alloc) {
@@ -811,16 +830,29 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
                        yrot_stride);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_OTI, s);
-    CrpBatch B{feats, track_off, track_len, NX, ldn, pb, w_oti, w_dims, m, tau, w_yrot, yrot_stride};
-    prof_begin(PH_SEL_ROWS, s);
-    if ((rc = run_select(false, st, B, nb, L, ld, params->kappa, w_thr_r, w_T_r, thr_stride, s))) return rc;
-    prof_end(PH_SEL_ROWS, s);
-    prof_begin(PH_SEL_COLS, s);
-    if ((rc = run_select(true, st, B, nb, L, ld, params->kappa, w_thr_c, w_T_c, thr_stride, s))) return rc;
-    prof_end(PH_SEL_COLS, s);
-    prof_begin(PH_MASK, s);
-    if ((rc = run_mask(st, B, nb, L, nstrips, w_T_r, w_T_c, thr_stride, w_mask, mask_stride, ld, s))) return rc;
-    prof_end(PH_MASK, s);
+    if (split) {
+      for (int s0 = 0; s0 < nb; s0 += (int)sub) {
+        const int ns = (nb - s0) < sub ? (nb - s0) : (int)sub;
+        CrpBatch Bs{feats, track_off, track_len, NX, ldn, pb + 2 * s0, w_oti + s0, w_dims + s0, m, tau,
+                    w_yrot + (size_t)s0 * yrot_stride, yrot_stride};
+        if ((rc = launch_crp_split(Bs, ns, L, params->kappa, w_kpl, ldk, kstride,
+                                   w_thr_r + (size_t)s0 * thr_stride, w_T_r + (size_t)s0 * thr_stride,
+                                   w_thr_c + (size_t)s0 * thr_stride, w_T_c + (size_t)s0 * thr_stride, thr_stride,
+                                   w_mask + (size_t)s0 * mask_stride, mask_stride, ld, s)))
+          return rc;
+      }
+    } else {
+      CrpBatch B{feats, track_off, track_len, NX, ldn, pb, w_oti, w_dims, m, tau, w_yrot, yrot_stride};
+      prof_begin(PH_SEL_ROWS, s);
+      if ((rc = run_select(false, st, B, nb, L, ld, params->kappa, w_thr_r, w_T_r, thr_stride, s))) return rc;
+      prof_end(PH_SEL_ROWS, s);
+      prof_begin(PH_SEL_COLS, s);
+      if ((rc = run_select(true, st, B, nb, L, ld, params->kappa, w_thr_c, w_T_c, thr_stride, s))) return rc;
+      prof_end(PH_SEL_COLS, s);
+      prof_begin(PH_MASK, s);
+      if ((rc = run_mask(st, B, nb, L, nstrips, w_T_r, w_T_c, thr_stride, w_mask, mask_stride, ld, s))) return rc;
+      prof_end(PH_MASK, s);
+    }
     if (qmax_out) {
       prof_begin(PH_DP_QMAX, s);
       launch_dp<0>(eqg, nb, w_mask, mask_stride, ld, w_dims, params->gamma_open, params->gamma_ext, w_bnd,

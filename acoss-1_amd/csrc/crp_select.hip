@@ -31,8 +31,6 @@ constexpr int kW = 256;                          // diagonals (= threads) per pa
 constexpr int kMS = 9;                           // frameStackSize of the fast path
 constexpr int kYRows = kW + kR + kMS - 2;        // 279 inner frames staged per panel
 constexpr int kNRows = kW + kR;                  // 272 inner norms staged per panel
-constexpr int kHist = 512;                       // bins of the per-wave histogram
-constexpr int kList = 64;                        // candidate list per wave (one per lane)
 
 struct SelCtx {
   const float* own;    // own frames (query, or the OTI-rolled reference in the TRANS pass)
@@ -158,17 +156,19 @@ __device__ __forceinline__ unsigned full_key_fast(const SelCtx& C, const float* 
 
 // ---- per-wave helpers ----
 
-// 16-bit prefix select: exact prefix P of the element of rank rho, #keys below P, #keys == P.
-struct Pref {
-  unsigned P;
-  int less, eq;
-};
+// Diagnostic stamps (ACOSS_DEBUG_STAMPS): wave 0 of each block adds the cycles of each
+// phase into dbg[0..7]. The branch is uniform; with dbg == nullptr no stamp executes.
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
 
-// Keys of one row as seen by one lane: lane l holds elements l + 64q. Two sources:
-// registers (rows up to 64*KPL keys, the common case) or the LDS row itself.
+// ---- per-row select on 16-bit key prefixes held in registers ----
+// Keys of one row as seen by one lane: lane l holds elements l + 64q (0xffffffff = none).
 template <int KPL>
 struct RowKeys {
-  unsigned v[KPL];  // 0xffffffff = no element
+  unsigned v[KPL];
   __device__ __forceinline__ void load(const uint16_t* row, int n) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -177,197 +177,99 @@ struct RowKeys {
       v[q] = e < n ? (unsigned)row[e] : 0xffffffffu;
     }
   }
-  template <typename F>
-  __device__ __forceinline__ void each(int n, F&& f) const {
-    const int lane = threadIdx.x & 63;
+  __device__ __forceinline__ int count_le(unsigned x) const {  // #keys <= x (x <= 0xffff)
+    int c = 0;
 #pragma unroll
-    for (int q = 0; q < KPL; ++q) f(v[q], lane + 64 * q);
+    for (int q = 0; q < KPL; ++q) c += v[q] <= x;
+    return wave_sum(c);
   }
-};
-
-struct LdsKeys {  // rows longer than 64*KPL: read straight from the LDS stripe
-  const uint16_t* row;
-  __device__ __forceinline__ void load(const uint16_t* r, int) { row = r; }
-  template <typename F>
-  __device__ __forceinline__ void each(int n, F&& f) const {
-    const int lane = threadIdx.x & 63;
-    for (int e = lane; e < n; e += 64) f((unsigned)row[e], e);
-    for (int e = n + lane; e < ((n + 63) & ~63); e += 64) f(0xffffffffu, e);
-  }
-};
-
-// Scan 512 (or 128) per-lane-octet histogram bins; the bin holding rank rho.
-__device__ __forceinline__ void scan_bins(const int* hist, int rho, int* bin, int* less, int* eq) {
-  const int lane = threadIdx.x & 63;
-  const int4* h4 = reinterpret_cast<const int4*>(hist);
-  const int4 c0 = h4[lane * 2], c1 = h4[lane * 2 + 1];
-  const int cnt[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-  int part = 0;
+  __device__ __forceinline__ void min_max(unsigned* mn, unsigned* mx) const {
+    unsigned a = 0xffffu, b = 0u;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) part += cnt[q];
-  const int incl = wave_incl_scan(part);
-  const int before = incl - part;
-  const bool mine = rho >= before && rho < incl;
-  int b = 0, l = 0, e = 0;
-  if (mine) {
-    int acc = before;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      if (rho >= acc && rho < acc + cnt[q]) {
-        b = lane * 8 + q;
-        l = acc;
-        e = cnt[q];
+    for (int q = 0; q < KPL; ++q) {
+      if (v[q] != 0xffffffffu) {
+        a = min(a, v[q]);
+        b = max(b, v[q]);
       }
-      acc += cnt[q];
     }
+    *mn = wave_min_u32(a);
+    *mx = wave_max_u32(b);
   }
-  const int src = __builtin_ctzll(__ballot(mine));
-  *bin = lane_bcast(b, src);
-  *less = lane_bcast(l, src);
-  *eq = lane_bcast(e, src);
-}
-
-__device__ __forceinline__ void clear_hist(int* hist) {
-  const int lane = threadIdx.x & 63;
-  int4* h4 = reinterpret_cast<int4*>(hist);
-  h4[lane * 2] = make_int4(0, 0, 0, 0);
-  h4[lane * 2 + 1] = make_int4(0, 0, 0, 0);
-  __builtin_amdgcn_wave_barrier();
-}
-
-template <typename K>
-__device__ Pref wave_prefix_select(const K& keys, int n, int rho, unsigned kmin, int shift, int* hist) {
-  clear_hist(hist);
-  keys.each(n, [&](unsigned v, int) {
-    if (v != 0xffffffffu) atomicAdd(&hist[(v - kmin) >> shift], 1);
-  });
-  __builtin_amdgcn_wave_barrier();
-  int bin, less, eq;
-  scan_bins(hist, rho, &bin, &less, &eq);
-  if (shift == 0) return Pref{kmin + (unsigned)bin, less, eq};
-  // pass B: low `shift` bits inside the bin (<= 128 bins)
-  __builtin_amdgcn_wave_barrier();
-  clear_hist(hist);
-  const unsigned lowmask = (1u << shift) - 1u;
-  keys.each(n, [&](unsigned v, int) {
-    const unsigned d = v - kmin;
-    if (v != 0xffffffffu && (d >> shift) == (unsigned)bin) atomicAdd(&hist[d & lowmask], 1);
-  });
-  __builtin_amdgcn_wave_barrier();
-  int sub, less2, eq2;
-  scan_bins(hist, rho - less, &sub, &less2, &eq2);
-  __builtin_amdgcn_wave_barrier();
-  return Pref{kmin + (((unsigned)bin << shift) | (unsigned)sub), less + less2, eq2};
-}
-
-// Full 32-bit keys of ranks rho1 <= rho2 (0-based) among the g cells of row `srow` whose
-// 16-bit prefix is P (one compaction + one exact recompute per member).
-template <bool TRANS, typename K>
-__device__ uint2 exact_in_group(const SelCtx& C, const K& keys, const uint16_t* row, const float* Xown, int n,
-                                int srow, unsigned P, int rho1, int rho2, int g, int* list) {
-  const int lane = threadIdx.x & 63;
-  if (g <= kList) {
+  __device__ __forceinline__ unsigned min_greater(unsigned x) const {
+    unsigned a = 0xffffffffu;
+#pragma unroll
+    for (int q = 0; q < KPL; ++q)
+      if (v[q] > x) a = min(a, v[q]);
+    return wave_min_u32(a);
+  }
+  // write the (row, column) of every key == P to list (wave-cooperative, ballot + mbcnt)
+  __device__ __forceinline__ void collect(unsigned P, int r, int* list) const {
+    const int lane = threadIdx.x & 63;
     int base = 0;
-    keys.each(n, [&](unsigned v, int e) {
-      const bool m = v == P;
+#pragma unroll
+    for (int q = 0; q < KPL; ++q) {
+      const bool m = v[q] == P;
       const unsigned long long bal = __ballot(m);
-      if (m) list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] = e;
+      if (m)
+        list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] =
+            (r << 16) | (lane + 64 * q);
       base += __popcll(bal);
-    });
-    __builtin_amdgcn_wave_barrier();
-    const bool act = lane < g;
-    const unsigned key = full_key_fast<TRANS>(C, Xown, srow, act ? list[lane] : 0, act);
-    int cl = 0, ce = 0;
-    for (int q = 0; q < g; ++q) {
-      const unsigned o = (unsigned)lane_bcast((int)key, q);
-      cl += o < key;
-      ce += o == key;
-    }
-    const int s1 = __builtin_ctzll(__ballot(act && cl <= rho1 && rho1 < cl + ce));
-    const int s2 = __builtin_ctzll(__ballot(act && cl <= rho2 && rho2 < cl + ce));
-    __builtin_amdgcn_wave_barrier();
-    return make_uint2((unsigned)lane_bcast((int)key, s1), (unsigned)lane_bcast((int)key, s2));
-  }
-  // large group (degenerate rows, e.g. long silences): MSB-first search on the low 16 bits,
-  // recomputing the members' exact keys at every step (plain loop over the LDS row).
-  unsigned res[2] = {0u, 0u};
-  const int rho[2] = {rho1, rho2};
-  for (int w = 0; w < 2; ++w) {
-    for (int b = 15; b >= 0; --b) {
-      const unsigned cand = res[w] | (1u << b);
-      int cnt = 0;
-      for (int e0 = 0; e0 < n; e0 += 64) {
-        const int e = e0 + lane;
-        const bool m = e < n && row[e] == (uint16_t)P;
-        if (__ballot(m)) {
-          const unsigned k = full_key<TRANS>(C, srow, m ? e : 0, m);
-          cnt += m && (k & 0xffffu) < cand;
-        }
-      }
-      cnt = wave_sum(cnt);
-      if (cnt <= rho[w]) res[w] = cand;
     }
   }
-  return make_uint2((P << 16) | res[0], (P << 16) | res[1]);
+};
+
+// Smallest prefix P with count(keys <= P) > rho (binary search over [kmin, kmax]).
+template <int KPL>
+__device__ __forceinline__ unsigned prefix_of_rank(const RowKeys<KPL>& K, int rho, unsigned kmin, unsigned kmax) {
+  unsigned a = kmin, b = kmax;
+  while (a < b) {
+    const unsigned mid = (a + b) >> 1;
+    if (K.count_le(mid) > rho)
+      b = mid;
+    else
+      a = mid + 1;
+  }
+  return a;
 }
 
-// Threshold of one row (own stacked frame srow) from its n 16-bit keys.
-template <bool TRANS, typename K>
-__device__ void row_threshold(const SelCtx& C, const K& keys, const uint16_t* row, const float* Xown, int n, int srow,
-                              float kappa, int* hist, int* list, float* thr_out, float* T_out, int ablate) {
+// Slow exact path for one group (very large prefix groups, e.g. long silences, or a full
+// candidate list): MSB-first search on the low 16 bits, recomputing member keys each step.
+template <bool TRANS>
+__device__ unsigned exact_slow(const SelCtx& C, const uint16_t* row, int n, int srow, unsigned P, int rho) {
   const int lane = threadIdx.x & 63;
-  const float q = (float)(n - 1) * kappa;
-  const float lo_f = floorf(q), hi_f = ceilf(q);
-  const int lo = (int)lo_f, hi = (int)hi_f;
-  unsigned kmin = 0xffffu, kmax = 0u;
-  keys.each(n, [&](unsigned v, int) {
-    if (v != 0xffffffffu) {
-      kmin = min(kmin, v);
-      kmax = max(kmax, v);
+  unsigned res = 0;
+  for (int b = 15; b >= 0; --b) {
+    const unsigned cand = res | (1u << b);
+    int cnt = 0;
+    for (int e0 = 0; e0 < n; e0 += 64) {
+      const int e = e0 + lane;
+      const bool m = e < n && row[e] == (uint16_t)P;
+      if (__ballot(m)) {
+        const unsigned k = full_key<TRANS>(C, srow, m ? e : 0, m);
+        cnt += m && (k & 0xffffu) < cand;
+      }
     }
-  });
-  kmin = wave_min_u32(kmin);
-  kmax = wave_max_u32(kmax);
-  int shift = 0;
-  while (((kmax - kmin) >> shift) >= (unsigned)kHist) ++shift;
-  if (ablate & 8) {  // debug: stop after min/max
-    if (lane == 0) thr_out[srow] = (float)(kmax - kmin);
-    return;
+    cnt = wave_sum(cnt);
+    if (cnt <= rho) res = cand;
   }
-  const Pref a = wave_prefix_select(keys, n, lo, kmin, shift, hist);
-  unsigned vlo, vhi;
-  if (ablate & 4) {  // debug: skip the exact phase
-    vlo = a.P << 16;
-    vhi = vlo;
-  } else if (hi == lo || hi < a.less + a.eq) {  // both order statistics share the 16-bit prefix
-    const uint2 v = exact_in_group<TRANS>(C, keys, row, Xown, n, srow, a.P, lo - a.less, hi - a.less, a.eq, list);
-    vlo = v.x;
-    vhi = v.y;
-  } else {  // hi is the smallest key of the next prefix group
-    vlo = exact_in_group<TRANS>(C, keys, row, Xown, n, srow, a.P, lo - a.less, lo - a.less, a.eq, list).x;
-    const Pref b = wave_prefix_select(keys, n, hi, kmin, shift, hist);
-    vhi = exact_in_group<TRANS>(C, keys, row, Xown, n, srow, b.P, hi - b.less, hi - b.less, b.eq, list).x;
-  }
-  if (lane == 0) {
-    const float slo = sqrt_rn(__builtin_bit_cast(float, vlo));
-    float thr;
-    if (lo_f == hi_f) {
-      thr = slo;
-    } else {
-      const float shi = sqrt_rn(__builtin_bit_cast(float, vhi));
-      const float aa = slo * (hi_f - q);
-      const float bb = shi * (q - lo_f);
-      thr = aa + bb;
-    }
-    thr_out[srow] = thr;
-    T_out[srow] = sq_threshold(thr);
-  }
+  return (P << 16) | res;
 }
+
+// Per-row bookkeeping between the phases (LDS).
+struct RowSel {
+  unsigned P[2];     // prefixes of the lo / hi order statistic
+  int rho[2];        // rank inside its prefix group
+  int off[2], g[2];  // candidate list slice (g == -1: slow path for that group, -2: whole row)
+};
+
+constexpr int kCand = 1024;  // block-wide candidate list capacity
 
 template <bool TRANS>
 __device__ __forceinline__ void select_body(const SelCtx& C, uint16_t* K16, float* Ys, float* Ns, float kappa, float* thr_out,
-                            float* T_out, int ablate) {
+                            float* T_out, int ablate, unsigned long long* dbg) {
   const int t = threadIdx.x;
+  unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
+  if (dbg) ts0 = stamp();
   // own stacked norms of the stripe: wave-uniform, loaded once (SGPRs)
   float nown[kR];
 #pragma unroll
@@ -441,38 +343,160 @@ __device__ __forceinline__ void select_body(const SelCtx& C, uint16_t* K16, floa
     }
   }
   __syncthreads();
-  // ---- per-wave selects ----
-  // own frames of the stripe into LDS (exact recompute of candidate cells)
+  if (dbg) ts1 = stamp();
+  // ---- selects ----
+  // LDS scratch (aliases the panel buffers): own frames | candidate list | row records | counter
   float* Xown = Ys;
+  int* cand = reinterpret_cast<int*>(Ys) + (kR + kMS - 1) * 12;
+  RowSel* rs = reinterpret_cast<RowSel*>(cand + kCand);
+  int* ncand = reinterpret_cast<int*>(rs + kR);
   for (int e = t; e < (kR + kMS - 1) * 12; e += kW) {
     const int a = e / 12, c = e - a * 12;
     int f = (C.i0 + a) * C.tau;
     f = f < C.n_own_f ? f : C.n_own_f - 1;
     Xown[e] = C.own[(size_t)f * 12 + c];
   }
+  if (t == 0) *ncand = 0;
   __syncthreads();
   const int lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform (SGPR)
-  int* hist = reinterpret_cast<int*>(Ys) + (kR + kMS - 1) * 12 + w * (kHist + kList);
-  int* list = hist + kHist;
   const int n = C.n_in_s;
-  for (int r = w; r < ((ablate & 2) ? 0 : C.rows); r += 4) {
+  const float q = (float)(n - 1) * kappa;
+  const float lo_f = floorf(q), hi_f = ceilf(q);
+  const int lo = (int)lo_f, hi = (int)hi_f;
+  const bool regs = n <= 64 * 32;
+  const int nrows = (ablate & 2) ? 0 : C.rows;
+  // phase A (per wave): 16-bit prefixes of both order statistics; candidates collected
+  for (int r = w; r < nrows; r += 4) {
     const uint16_t* row = K16 + r * C.ld16;
-    const int srow = __builtin_amdgcn_readfirstlane(C.i0 + r);
-    if (n <= 64 * 32) {
-      RowKeys<32> keys;
-      keys.load(row, n);
-      row_threshold<TRANS>(C, keys, row, Xown, n, srow, kappa, hist, list, thr_out, T_out, ablate);
+    RowSel sel;
+    if (regs) {
+      RowKeys<32> K;
+      K.load(row, n);
+      unsigned kmin, kmax;
+      K.min_max(&kmin, &kmax);
+      const unsigned Pl = prefix_of_rank(K, lo, kmin, kmax);
+      const int le = K.count_le(Pl);
+      const int less = Pl > 0 ? K.count_le(Pl - 1) : 0;
+      sel.P[0] = Pl;
+      sel.rho[0] = lo - less;
+      sel.g[0] = le - less;
+      if (hi < le) {  // hi shares the prefix group of lo
+        sel.P[1] = Pl;
+        sel.rho[1] = hi - less;
+        sel.g[1] = sel.g[0];
+      } else {  // hi = smallest key of the next group
+        const unsigned Ph = K.min_greater(Pl);
+        sel.P[1] = Ph;
+        sel.rho[1] = 0;
+        sel.g[1] = K.count_le(Ph) - le;
+      }
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && sel.P[1] == sel.P[0]) {
+          sel.off[1] = sel.off[0];
+          sel.g[1] = sel.g[0];
+          continue;
+        }
+        int off = -1;
+        if (sel.g[h] <= 64 && lane == 0) off = atomicAdd(ncand, sel.g[h]);
+        off = lane_bcast(off, 0);
+        if (off >= 0 && off + sel.g[h] <= kCand) {
+          K.collect(sel.P[h], r, cand + off);
+          sel.off[h] = off;
+        } else {
+          sel.off[h] = -1;
+          sel.g[h] = -1;  // slow path for this group
+        }
+      }
     } else {
-      LdsKeys keys;
-      keys.load(row, n);
-      row_threshold<TRANS>(C, keys, row, Xown, n, srow, kappa, hist, list, thr_out, T_out, ablate);
+      sel.g[0] = sel.g[1] = -2;  // long rows: fully slow path in phase C
+    }
+    if (lane == 0) rs[r] = sel;
+  }
+  __syncthreads();
+  if (dbg) ts2 = stamp();
+  // phase B (block): exact keys of every collected candidate, one per thread, in one round
+  const int nc = min(*ncand, kCand);
+  for (int e = t; e < nc; e += kW) {
+    const int pk = cand[e];
+    const int r = pk >> 16, j = pk & 0xffff;
+    cand[e] = (int)full_key_fast<TRANS>(C, Xown, C.i0 + r, j, true);
+  }
+  __syncthreads();
+  if (dbg) ts3 = stamp();
+  // phase C (per wave): rank inside the groups, interpolate, squared-domain threshold
+  for (int r = w; r < nrows; r += 4) {
+    const int srow = __builtin_amdgcn_readfirstlane(C.i0 + r);
+    const RowSel sel = rs[r];
+    const uint16_t* row = K16 + r * C.ld16;
+    unsigned v[2];
+    if (sel.g[0] == -2) {  // long row: count-based search straight from LDS (slow, rare)
+      for (int h = 0; h < 2; ++h) {
+        const int rho = h == 0 ? lo : hi;
+        unsigned a = 0, b = 0xffffu;
+        while (a < b) {
+          const unsigned mid = (a + b) >> 1;
+          int c = 0;
+          for (int e = lane; e < n; e += 64) c += row[e] <= mid;
+          if (wave_sum(c) > rho)
+            b = mid;
+          else
+            a = mid + 1;
+        }
+        int less = 0;
+        for (int e = lane; e < n; e += 64) less += row[e] < a;
+        less = wave_sum(less);
+        v[h] = exact_slow<TRANS>(C, row, n, srow, a, rho - less);
+      }
+    } else {
+      for (int h = 0; h < 2; ++h) {
+        if (sel.g[h] < 0) {
+          v[h] = exact_slow<TRANS>(C, row, n, srow, sel.P[h], sel.rho[h]);
+          continue;
+        }
+        const int g = sel.g[h];
+        const unsigned key = lane < g ? (unsigned)cand[sel.off[h] + lane] : 0xffffffffu;
+        int cl = 0, ce = 0;
+        for (int qq = 0; qq < g; ++qq) {
+          const unsigned o = (unsigned)lane_bcast((int)key, qq);
+          cl += o < key;
+          ce += o == key;
+        }
+        const int src = __builtin_ctzll(__ballot(lane < g && cl <= sel.rho[h] && sel.rho[h] < cl + ce));
+        v[h] = (unsigned)lane_bcast((int)key, src);
+      }
+    }
+    if (lane == 0) {
+      const float slo = sqrt_rn(__builtin_bit_cast(float, v[0]));
+      float thr;
+      if (lo_f == hi_f) {
+        thr = slo;
+      } else {
+        const float shi = sqrt_rn(__builtin_bit_cast(float, v[1]));
+        const float aa = slo * (hi_f - q);
+        const float bb = shi * (q - lo_f);
+        thr = aa + bb;
+      }
+      thr_out[srow] = thr;
+      T_out[srow] = sq_threshold(thr);
+    }
+  }
+  if (dbg) {
+    __syncthreads();
+    const unsigned long long ts4 = stamp();
+    if (t == 0) {
+      atomicAdd(dbg + 0, ts1 - ts0);
+      atomicAdd(dbg + 1, ts2 - ts1);
+      atomicAdd(dbg + 2, ts3 - ts2);
+      atomicAdd(dbg + 3, ts4 - ts3);
+      atomicAdd(dbg + 4, 1ull);
     }
   }
 }
 
 template <bool TRANS>
 __global__ __launch_bounds__(256, 2) void k_crp_select16(CrpBatch B, int ld16, float kappa, float* __restrict__ thr,
-                                                         float* __restrict__ Tq, int64_t thr_stride, int ablate) {
+                                                         float* __restrict__ Tq, int64_t thr_stride, int ablate,
+                                                         unsigned long long* dbg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem8[];
   const int p = blockIdx.y;
   const int2 dm = B.dims[p];
@@ -498,11 +522,11 @@ __global__ __launch_bounds__(256, 2) void k_crp_select16(CrpBatch B, int ld16, f
   uint16_t* K16 = reinterpret_cast<uint16_t*>(smem8);
   float* Ys = reinterpret_cast<float*>(smem8 + align_up((size_t)kR * ld16 * 2, 16));
   float* Ns = Ys + kYRows * 12;
-  select_body<TRANS>(C, K16, Ys, Ns, kappa, thr + (size_t)p * thr_stride, Tq + (size_t)p * thr_stride, ablate);
+  select_body<TRANS>(C, K16, Ys, Ns, kappa, thr + (size_t)p * thr_stride, Tq + (size_t)p * thr_stride, ablate, dbg);
 }
 
 size_t select16_lds(int ld16) {
-  const size_t scratch = (size_t)(kR + kMS - 1) * 12 * 4 + (size_t)4 * (kHist + kList) * 4;
+  const size_t scratch = (size_t)(kR + kMS - 1) * 12 * 4 + (size_t)kCand * 4 + sizeof(RowSel) * kR + 16;
   const size_t panel = (size_t)kYRows * 12 * 4 + (size_t)kNRows * 4;
   return align_up((size_t)kR * ld16 * 2, 16) + (panel > scratch ? panel : scratch);
 }
@@ -520,12 +544,24 @@ int launch_select16(bool trans, const CrpBatch& B, int nb, int L, float kappa, f
   if (lds > 64 * 1024) ACOSS_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const dim3 grid((L + kR - 1) / kR, nb);
   static const int ablate = getenv("ACOSS_DEBUG_ABLATE") ? atoi(getenv("ACOSS_DEBUG_ABLATE")) : 0;
+  unsigned long long* dbg = nullptr;
+  if (getenv("ACOSS_DEBUG_STAMPS")) dbg = static_cast<unsigned long long*>(workspace(9, 256));
   if (trans)
-    hipLaunchKernelGGL(k_crp_select16<true>, grid, dim3(256), lds, s, B, ld16, kappa, thr, T, thr_stride, ablate);
+    hipLaunchKernelGGL(k_crp_select16<true>, grid, dim3(256), lds, s, B, ld16, kappa, thr, T, thr_stride, ablate, dbg);
   else
-    hipLaunchKernelGGL(k_crp_select16<false>, grid, dim3(256), lds, s, B, ld16, kappa, thr, T, thr_stride, ablate);
+    hipLaunchKernelGGL(k_crp_select16<false>, grid, dim3(256), lds, s, B, ld16, kappa, thr, T, thr_stride, ablate, dbg);
   ACOSS_LAUNCH_CHECK();
   return ACOSS_OK;
 }
 
 }  // namespace acoss
+
+// Diagnostic: read and clear the stamp sums (ACOSS_DEBUG_STAMPS builds only).
+extern "C" int acoss_debug_stamps(unsigned long long* out8) {
+  void* d = acoss::workspace(9, 256);
+  if (!d) return ACOSS_E_HIP;
+  if (hipDeviceSynchronize() != hipSuccess) return ACOSS_E_HIP;
+  if (hipMemcpy(out8, d, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return ACOSS_E_HIP;
+  if (hipMemset(d, 0, 256) != hipSuccess) return ACOSS_E_HIP;
+  return ACOSS_OK;
+}

@@ -66,3 +66,54 @@ def test_align_crp_rejects_nonbinary():
     C[3, 4] = 2
     with pytest.raises(_lib.AcossHipError):
         _lib.align_crp(C)
+
+
+@pytest.mark.parametrize("M,N,silence", [(400, 380, (50, 250)), (2300, 2210, None), (2100, 2300, (100, 700))])
+def test_crp_pair_degenerate_rows(M, N, silence):
+    """Long silences (huge groups of equal / zero keys) and rows longer than 2048 cells
+    exercise the slow exact paths of the threshold select."""
+    rng = np.random.Generator(np.random.PCG64(M + N))
+    X, Y = _pair(rng, M, N)
+    if silence:
+        a, b = silence
+        X[a:b] = 0.0
+        Y[a:b] = 0.0
+    ref = oracle.crp_pair(X, Y)
+    got = _lib.crp_pair(X, Y, _lib.crp_params())
+    np.testing.assert_array_equal(got["thr_row"].cpu().numpy().view(np.uint32), ref["thr_row"].view(np.uint32))
+    np.testing.assert_array_equal(got["thr_col"].cpu().numpy().view(np.uint32), ref["thr_col"].view(np.uint32))
+    np.testing.assert_array_equal(got["crp"].cpu().numpy(), ref["crp"])
+
+
+@pytest.mark.parametrize("path", ["split", "fused"])
+def test_crp_align_degenerate_batch(path, monkeypatch):
+    """Batch path on silences / ragged lengths / long tracks, both CRP implementations."""
+    import subprocess
+    import sys
+    import os
+    code = r'''
+import sys, numpy as np
+sys.path[:0] = [%r, %r]
+import oracle
+from acoss import _lib, synthetic
+rng = np.random.Generator(np.random.PCG64(99))
+tracks = []
+for n in [120, 400, 2055, 1500, 37, 900]:
+    b = synthetic.base_sequence(rng, n)
+    x = synthetic.render(rng, b)
+    if n >= 400:
+        x[50:300] = 0.0
+    tracks.append(x)
+feats, off, lens = synthetic.pack(tracks)
+pairs = np.array([(i, j) for i in range(len(tracks)) for j in range(len(tracks)) if i != j], np.int32)
+q, d, k = oracle.crp_batch(feats, off, lens, pairs)
+got = _lib.crp_align(feats, off, lens, int(lens.max()), pairs, _lib.crp_params(), qmax=True, dmax=True, oti=True)
+assert np.array_equal(got["oti"].cpu().numpy(), k)
+assert np.array_equal(got["qmax"].cpu().numpy(), q), (got["qmax"].cpu().numpy(), q)
+assert np.array_equal(got["dmax"].cpu().numpy(), d)
+print("ok")
+''' % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+       os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "acoss-1_amd"))
+    env = dict(os.environ, ACOSS_CRP_PATH=path)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
