@@ -63,6 +63,9 @@ def load_library(path=None):
         raise AcossHipError(
             "libacoss_hip.so not found at %s: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(or `make -C acoss-1_amd/csrc`). There is no CPU fallback." % p)
+    # torch bundles its own libamdhip64.so.7 (same soname as /opt/rocm's): load it first so
+    # this library binds to the runtime torch's allocator and streams live in
+    import torch  # noqa: F401
     lib = ctypes.CDLL(p)
     for name, argt in SIGNATURES.items():
         fn = getattr(lib, name)
@@ -173,6 +176,133 @@ def align_crp(C, align=0, gamma_open=0.5, gamma_ext=0.5):
                              float(gamma_ext), _ptr(out), _stream())
     _check(rc, "acoss_align_crp")
     return out
+
+
+def _pack_mats(mats, dtype):
+    """list of 2-D arrays -> (flat device buffer, offsets i64, rows i32, cols i32, max_rows, max_cols)."""
+    torch = _torch()
+    shapes = [tuple(int(v) for v in m.shape) for m in mats]
+    sizes = [r * c for r, c in shapes]
+    off = np.zeros(len(mats), dtype=np.int64)
+    if len(mats) > 1:
+        off[1:] = np.cumsum(sizes[:-1])
+    flat = torch.empty(max(1, int(sum(sizes))), dtype=dtype, device="cuda")
+    for m, o, n in zip(mats, off, sizes):
+        if n:
+            flat[int(o):int(o) + n] = _dev(m, dtype).reshape(-1)
+    rows = np.array([r for r, _ in shapes], dtype=np.int32)
+    cols = np.array([c for _, c in shapes], dtype=np.int32)
+    return (flat, _dev(off, torch.int64), _dev(rows, torch.int32), _dev(cols, torch.int32),
+            int(rows.max(initial=0)), int(cols.max(initial=0)))
+
+
+def _as_binary_u8(m):
+    """Binary matrix -> uint8, raising like `match` (alignment_tools.py:17-23) on other values."""
+    torch = _torch()
+    t = m if isinstance(m, torch.Tensor) else torch.as_tensor(np.asarray(m))
+    if t.dtype not in (torch.uint8, torch.bool):
+        t = t.to("cuda")
+        if bool(((t != 0) & (t != 1)).any()):
+            raise IOError("Non-binary elements found in input")
+    return t.to(device="cuda", dtype=torch.uint8)
+
+
+def sw_constrained(mats):
+    """smith_waterman_constrained (alignment_tools.py:27-46) of a list of binary matrices -> (n,) f64."""
+    torch = _torch()
+    lib = load_library()
+    mats = [_as_binary_u8(m) for m in mats]
+    out = torch.empty(len(mats), dtype=torch.float64, device="cuda")
+    if not mats:
+        return out
+    flat, off, rows, cols, mr, mc = _pack_mats(mats, torch.uint8)
+    rc = lib.acoss_sw_constrained(_ptr(flat), _ptr(off), _ptr(rows), _ptr(cols), len(mats), mr, mc, _ptr(out),
+                                  _stream())
+    if rc == -4:
+        raise IOError("Non-binary elements found in input")
+    _check(rc, "acoss_sw_constrained")
+    return out
+
+
+CSM_KINDS = {"euclidean": 0, "euclid": 0, "cosine": 1, "ssm": 2}
+
+
+def csm(X, Y=None, kind="euclidean", oti_shift=0):
+    """get_csm / get_csm_cosine / get_ssm (cross_recurrence.py:10-73); oti_shift > 0 rolls each
+    12-bin block of X first (get_csm_blocked_oti, :105-134). float32 (M, N) device tensor."""
+    torch = _torch()
+    lib = load_library()
+    k = CSM_KINDS[kind]
+    X = _dev(X, torch.float32)
+    if X.dim() != 2:
+        raise ValueError("X must be 2-D")
+    if k == 2:
+        Yt, N = None, X.shape[0]
+    else:
+        Yt = _dev(Y, torch.float32)
+        if Yt.dim() != 2 or Yt.shape[1] != X.shape[1]:
+            raise ValueError("X and Y need the same feature dimension")
+        N = Yt.shape[0]
+    out = torch.empty((X.shape[0], N), dtype=torch.float32, device="cuda")
+    rc = lib.acoss_csm(_ptr(X), int(X.shape[0]), _ptr(Yt), int(N), int(X.shape[1]), k, int(oti_shift), _ptr(out),
+                       _stream())
+    _check(rc, "acoss_csm")
+    return out
+
+
+def get_oti(C1, C2):
+    """get_oti (cross_recurrence.py:75-103) for (n, 12) batches (or single (12,) vectors)."""
+    torch = _torch()
+    lib = load_library()
+    a = _dev(C1, torch.float32).reshape(-1, 12)
+    b = _dev(C2, torch.float32).reshape(-1, 12)
+    out = torch.empty(a.shape[0], dtype=torch.int32, device="cuda")
+    rc = lib.acoss_get_oti(_ptr(a), _ptr(b), int(a.shape[0]), _ptr(out), _stream())
+    _check(rc, "acoss_get_oti")
+    return out
+
+
+def binarize_rows(D, nneighbs):
+    """The nneighbs smallest of every row -> 1 (csm_to_binary, cross_recurrence.py:136-161)."""
+    torch = _torch()
+    lib = load_library()
+    D = _dev(D, torch.float32)
+    out = torch.empty(D.shape, dtype=torch.uint8, device="cuda")
+    rc = lib.acoss_binarize_rows(_ptr(D), int(D.shape[0]), int(D.shape[1]), int(nneighbs), _ptr(out), _stream())
+    _check(rc, "acoss_binarize_rows")
+    return out
+
+
+def wcsm(CSM, k1, k2, mu=0.5):
+    """getWCSM (similarity_fusion.py:38-54)."""
+    torch = _torch()
+    lib = load_library()
+    C = _dev(CSM, torch.float32)
+    out = torch.empty(C.shape, dtype=torch.float32, device="cuda")
+    rc = lib.acoss_wcsm(_ptr(C), int(C.shape[0]), int(C.shape[1]), int(k1), int(k2), float(mu), _ptr(out), _stream())
+    _check(rc, "acoss_wcsm")
+    return out
+
+
+def simple_mp(feats, pairs, sslen=10):
+    """SiMPle median matrix-profile distance (simple_silva.py:45-118) of ordered pairs.
+    feats: list of (12, n) float64 arrays; pairs (P, 2) (query, reference).
+    Returns (score f64 (P,), oti i32 (P,)) device tensors; the reference stores -score."""
+    torch = _torch()
+    lib = load_library()
+    mats = [np.asarray(f) if not isinstance(f, torch.Tensor) else f for f in feats]
+    for f in mats:
+        if f.shape[0] != 12:
+            raise ValueError("SiMPle features are (12, n) blocks")
+    flat, off, rows, cols, _, ml = _pack_mats(mats, torch.float64)
+    pairs = _dev(pairs, torch.int32).reshape(-1, 2)
+    P = pairs.shape[0]
+    score = torch.empty(P, dtype=torch.float64, device="cuda")
+    oti = torch.empty(P, dtype=torch.int32, device="cuda")
+    rc = lib.acoss_simple_mp(_ptr(flat), _ptr(off), _ptr(cols), len(mats), ml, _ptr(pairs), int(P), int(sslen),
+                             _ptr(score), _ptr(oti), _stream())
+    _check(rc, "acoss_simple_mp")
+    return score, oti
 
 
 def profile_enable(on=True):

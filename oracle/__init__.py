@@ -59,6 +59,8 @@ def lib():
         L.or_simple_sim.argtypes = [_dp, ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int]
         L.or_track_profile.argtypes = [_fp, ctypes.c_int, _fp]
         L.or_oti.argtypes = [_fp, _fp]
+        L.or_simple_oti.restype = ctypes.c_int
+        L.or_simple_oti.argtypes = [_dp, ctypes.c_int, _dp, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -144,3 +146,10 @@ def oti(pq, pr):
     pq = np.ascontiguousarray(pq, np.float32)
     pr = np.ascontiguousarray(pr, np.float32)
     return int(lib().or_oti(_p(pq, _fp), _p(pr, _fp)))
+
+
+def simple_oti(A, B):
+    """Simple.oti index (simple_silva.py:45-54) of two (12, n) float64 blocks."""
+    A = np.ascontiguousarray(A, np.float64)
+    B = np.ascontiguousarray(B, np.float64)
+    return int(lib().or_simple_oti(_p(A, _dp), A.shape[1], _p(B, _dp), B.shape[1]))

@@ -326,4 +326,29 @@ double or_simple_sim(const double* A, int na, const double* B, int nb, int L) {
   return (P % 2) ? mp[P / 2] : 0.5 * (mp[P / 2 - 1] + mp[P / 2]);
 }
 
+// Simple.oti (acoss/algorithms/simple_silva.py:45-54): profiles are per-bin sums over time
+// (sequential), v[k] = <p_a, roll(p_b, k)> (sequential), k* = argsort(v)[-1]: numpy's
+// small-array sort is stable, so among equal maxima the last index wins.
+int or_simple_oti(const double* A, int na, const double* B, int nb) {
+  double pa[12], pb[12];
+  for (int c = 0; c < 12; ++c) {
+    double x = 0.0, y = 0.0;
+    for (int t = 0; t < na; ++t) x += A[(size_t)c * na + t];
+    for (int t = 0; t < nb; ++t) y += B[(size_t)c * nb + t];
+    pa[c] = x;
+    pb[c] = y;
+  }
+  int best = 0;
+  double bv = 0.0;
+  for (int k = 0; k < 12; ++k) {
+    double acc = 0.0;
+    for (int c = 0; c < 12; ++c) acc += pa[c] * pb[(c - k + 12) % 12];
+    if (k == 0 || acc >= bv) {
+      bv = acc;
+      best = k;
+    }
+  }
+  return best;
+}
+
 }  // extern "C"

@@ -8,5 +8,8 @@ for p in (ROOT, os.path.join(ROOT, "acoss-1_amd")):
         sys.path.insert(0, p)
 
 
+GOLDEN = os.path.join(ROOT, "tests", "golden", "reference_golden.npz")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP) GPU; run with -m gpu")
