@@ -44,7 +44,9 @@ SIGNATURES = {
     "acoss_get_oti": [_vp, _vp, _i32, _vp, _vp],
     "acoss_binarize_rows": [_vp, _i32, _i32, _i32, _vp, _vp],
     "acoss_wcsm": [_vp, _i32, _i32, _i32, _i32, _f32, _vp, _vp],
-    "acoss_simple_mp": [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _i32, _vp, _vp, _vp],
+    "acoss_simple_mp": [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _vp],
+    "acoss_median_downsample": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
+    "acoss_simple_features": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _i64, _vp],
     "acoss_release_workspace": [],
     "acoss_profile_enable": [ctypes.c_int],
     "acoss_profile_read": [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int],
@@ -112,6 +114,12 @@ def _dev(x, dtype):
     return torch.as_tensor(np.ascontiguousarray(x)).to(device="cuda", dtype=dtype).contiguous()
 
 
+def _check_pairs(pairs, n_tracks):
+    """Host-side bounds check of (P, 2) track indices before a kernel dereferences them."""
+    if pairs.numel() and (int(pairs.min()) < 0 or int(pairs.max()) >= n_tracks):
+        raise ValueError("pair indices must lie in [0, %d)" % n_tracks)
+
+
 def crp_params(m=9, tau=1, kappa=0.095, oti=True, gamma_open=0.5, gamma_ext=0.5):
     return CrpParams(int(m), int(tau), float(kappa), int(bool(oti)), float(gamma_open), float(gamma_ext))
 
@@ -127,7 +135,8 @@ def crp_align(feats, track_off, track_len, max_len, pairs, params, qmax=True, dm
     feats = _dev(feats, torch.float32)
     track_off = _dev(track_off, torch.int64)
     track_len = _dev(track_len, torch.int32)
-    pairs = _dev(pairs, torch.int32)
+    pairs = _dev(pairs, torch.int32).reshape(-1, 2)
+    _check_pairs(pairs, int(track_len.shape[0]))
     P = pairs.shape[0]
     out = {}
     q = torch.empty(P, dtype=torch.float32, device="cuda") if qmax else None
@@ -284,25 +293,91 @@ def wcsm(CSM, k1, k2, mu=0.5):
     return out
 
 
-def simple_mp(feats, pairs, sslen=10):
+def simple_mp_packed(flat, track_off, track_len, pairs, sslen=10, apply_oti=True):
+    """SiMPle over packed (12 x n_t) float64 blocks: flat device buffer, element offsets,
+    lengths (columns). Returns (score f64 (P,), oti i32 (P,)) device tensors."""
+    torch = _torch()
+    lib = load_library()
+    lens = np.asarray(track_len.cpu() if isinstance(track_len, torch.Tensor) else track_len, np.int64)
+    pairs = _dev(pairs, torch.int32).reshape(-1, 2)
+    _check_pairs(pairs, len(lens))
+    P = pairs.shape[0]
+    score = torch.empty(P, dtype=torch.float64, device="cuda")
+    oti = torch.empty(P, dtype=torch.int32, device="cuda")
+    # keep every device buffer referenced until the launch is queued: a temporary passed as
+    # _ptr(_dev(...)) returns to torch's caching allocator at once and can be reused
+    flat_d = _dev(flat, torch.float64)
+    off_d = _dev(track_off, torch.int64)
+    len_d = _dev(lens.astype(np.int32), torch.int32)
+    rc = lib.acoss_simple_mp(_ptr(flat_d), _ptr(off_d), _ptr(len_d), len(lens), int(lens.max(initial=0)),
+                             _ptr(pairs), int(P), int(sslen), int(bool(apply_oti)), _ptr(score), _ptr(oti), _stream())
+    _check(rc, "acoss_simple_mp")
+    return score, oti
+
+
+def simple_mp(feats, pairs, sslen=10, apply_oti=True):
     """SiMPle median matrix-profile distance (simple_silva.py:45-118) of ordered pairs.
     feats: list of (12, n) float64 arrays; pairs (P, 2) (query, reference).
     Returns (score f64 (P,), oti i32 (P,)) device tensors; the reference stores -score."""
     torch = _torch()
-    lib = load_library()
     mats = [np.asarray(f) if not isinstance(f, torch.Tensor) else f for f in feats]
     for f in mats:
         if f.shape[0] != 12:
             raise ValueError("SiMPle features are (12, n) blocks")
-    flat, off, rows, cols, _, ml = _pack_mats(mats, torch.float64)
-    pairs = _dev(pairs, torch.int32).reshape(-1, 2)
-    P = pairs.shape[0]
-    score = torch.empty(P, dtype=torch.float64, device="cuda")
-    oti = torch.empty(P, dtype=torch.int32, device="cuda")
-    rc = lib.acoss_simple_mp(_ptr(flat), _ptr(off), _ptr(cols), len(mats), ml, _ptr(pairs), int(P), int(sslen),
-                             _ptr(score), _ptr(oti), _stream())
-    _check(rc, "acoss_simple_mp")
-    return score, oti
+    flat, off, _, cols, _, _ = _pack_mats(mats, torch.float64)
+    return simple_mp_packed(flat, off, cols, pairs, sslen, apply_oti)
+
+
+def median_downsample(feats, track_off, track_len, factor=40):
+    """librosa.util.sync(chroma.T, arange(0, n, factor), aggregate=np.median).T per track
+    (rqa_serra09.py:44-53). Returns (out (sum ceil(n/f), 12) f32 device, out_off i64, out_len i32)."""
+    torch = _torch()
+    lib = load_library()
+    lens = np.asarray(track_len.cpu() if isinstance(track_len, torch.Tensor) else track_len, np.int64)
+    out_len = (lens + factor - 1) // factor
+    out_off = np.zeros(len(lens), np.int64)
+    if len(lens) > 1:
+        out_off[1:] = np.cumsum(out_len[:-1])
+    out = torch.empty((max(1, int(out_len.sum())), 12), dtype=torch.float32, device="cuda")
+    f = _dev(feats, torch.float32)
+    o = _dev(track_off, torch.int64)
+    ln = _dev(lens.astype(np.int32), torch.int32)
+    oo = _dev(out_off, torch.int64)
+    rc = lib.acoss_median_downsample(_ptr(f), _ptr(o), _ptr(ln), len(lens), int(lens.max(initial=0)), int(factor),
+                                     _ptr(out), _ptr(oo), _stream())
+    _check(rc, "acoss_median_downsample")
+    return out[: int(out_len.sum())], out_off, out_len.astype(np.int32)
+
+
+def hann_smoothing(win_len_smooth=4):
+    """Simple.smooth's window: scipy/librosa get_window('hann', L + 2, fftbins=False), sum 1."""
+    from scipy import signal
+    w = signal.get_window("hann", win_len_smooth + 2, fftbins=False)
+    return np.ascontiguousarray(w / np.sum(w), np.float64)
+
+
+def simple_features(feats, track_off, track_len, win=200, skip=100, win_len_smooth=4):
+    """Simple.load_features for every track (simple_silva.py:34-43,56-66).
+    Returns (out flat f64 device, out_off i64 (element offsets), T i32 (columns per track));
+    track t is out[out_off[t]: out_off[t] + 12*T[t]].view(12, T[t])."""
+    torch = _torch()
+    lib = load_library()
+    lens = np.asarray(track_len.cpu() if isinstance(track_len, torch.Tensor) else track_len, np.int64)
+    T = lens // skip
+    out_off = np.zeros(len(lens), np.int64)
+    if len(lens) > 1:
+        out_off[1:] = np.cumsum(12 * T[:-1])
+    total = int(12 * T.sum())
+    out = torch.empty(max(1, total), dtype=torch.float64, device="cuda")
+    w = hann_smoothing(win_len_smooth)
+    f = _dev(feats, torch.float32)
+    o = _dev(track_off, torch.int64)
+    ln = _dev(lens.astype(np.int32), torch.int32)
+    oo = _dev(out_off, torch.int64)
+    rc = lib.acoss_simple_features(_ptr(f), _ptr(o), _ptr(ln), len(lens), int(win), int(skip),
+                                   w.ctypes.data_as(ctypes.c_void_p), len(w), _ptr(out), _ptr(oo), total, _stream())
+    _check(rc, "acoss_simple_features")
+    return out[:total], out_off, T.astype(np.int32)
 
 
 def profile_enable(on=True):

@@ -1,0 +1,182 @@
+"""CoverAlgorithm — the plugin base class (acoss/algorithms/algorithm_template.py), MI355X engine.
+
+The public surface is the reference's: constructor arguments, `filepaths`, `cliques`, `N`,
+`Ds` (float32 N x N memmaps at '<cachedir>/<name>_<shortname>_<type>_dmat'),
+`load_features(i)`, `get_all_clique_ids()`, `similarity(idxs)`, `all_pairwise(parallel,
+n_cores, symmetric, precomputed)`, `cleanup_memmap()`, `getEvalStatistics(type, topsidx)`.
+
+What changes is how the pair loop runs (algorithm_template.py:142-193). The reference calls
+`similarity` on one pair (serial) or on 45 chunks (joblib processes). Here:
+  * `prepare()` loads every track once (clique bookkeeping in index order, as the serial
+    reference does) and lets the subclass build its device-resident banks;
+  * the pairs, in the reference's enumeration order (combinations / permutations), go to
+    `similarity` in large chunks; the subclasses score a chunk with one batched HIP call;
+  * with torch.distributed initialised (one process per GPU, RCCL), every rank scores one
+    cost-balanced row stripe (acoss.distributed) and ONE all-gather assembles Ds on every
+    rank; `parallel` / `n_cores` are accepted for signature compatibility and ignored;
+  * Ds is saved as '<prefix>_Ds.npz' (deepdish/h5py are absent; `precomputed=True` reads it
+    back, or the reference's '<prefix>_Ds.h5' when h5py is importable).
+Reference defects not reproduced: the NameError of parallel=True at
+:174-192 and `cleanup_memmap` calling rmtree on files (:202).
+"""
+import os
+import warnings
+
+import numpy as np
+
+from .. import distributed as _dist
+from .. import evaluation
+from ..features_io import load_features as _load_feature_file
+from ..utils import create_dataset_filepaths
+
+__all__ = ["CoverAlgorithm"]
+
+PAIR_CHUNK = 1 << 20  # pairs per similarity() call (the engine batches further inside)
+
+
+def _dist_info():
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size(), dist.get_rank()
+    except ImportError:
+        pass
+    return 1, 0
+
+
+class CoverAlgorithm(object):
+    def __init__(self, dataset_csv, name="Serra09", datapath="features_benchmark", shortname="full",
+                 cachedir="cache", similarity_types=["main"]):
+        self.name = name
+        self.shortname = shortname
+        self.cachedir = cachedir
+        self.filepaths = create_dataset_filepaths(dataset_csv, root_audio_dir=datapath, file_format=".h5")
+        self.cliques = {}
+        self.N = len(self.filepaths)
+        os.makedirs(cachedir, exist_ok=True)
+        self.Ds = {}
+        for s in similarity_types:
+            self.Ds[s] = np.memmap("%s_%s_dmat" % (self.get_cacheprefix(), s), shape=(self.N, self.N), mode="w+",
+                                   dtype="float32")
+        self._prepared = False
+        print("Initialized %s algorithm on %i songs in dataset %s" % (name, self.N, shortname))
+
+    # ------------------------------------------------------------------ features
+    def get_cacheprefix(self):
+        return "%s/%s_%s" % (self.cachedir, self.name, self.shortname)
+
+    def load_features(self, i):
+        """Feature dict of song i; records its clique as a side effect (:70-94)."""
+        feats = _load_feature_file(self.filepaths[i])
+        label = feats["label"]
+        if label not in self.cliques:
+            self.cliques[label] = set([])
+        self.cliques[label].add(i)
+        return feats
+
+    def get_all_clique_ids(self, verbose=False):
+        """Clique membership of every song, cached in '<prefix>_clique_info.txt' (:96-119)."""
+        path = "%s_clique_info.txt" % self.get_cacheprefix()
+        if not os.path.exists(path):
+            with open(path, "w") as fout:
+                for i in range(len(self.filepaths)):
+                    feats = CoverAlgorithm.load_features(self, i)
+                    if verbose:
+                        print(i)
+                    fout.write("%i,%s\n" % (i, feats["label"]))
+        else:
+            with open(path) as fin:
+                for line in fin.readlines():
+                    i, label = line.split(",")
+                    label = label.strip()
+                    self.cliques.setdefault(label, set([])).add(int(i))
+
+    def prepare(self):
+        """Load every song once (index order) and build the subclass's device banks."""
+        if not self._prepared:
+            for i in range(self.N):
+                self.load_features(i)
+            self._prepared = True
+
+    def track_lengths(self):
+        """Per-song cost proxy for the stripe balance (frames at the pair kernel's input)."""
+        return np.ones(self.N, np.int64) * 100
+
+    # ------------------------------------------------------------------ pairs
+    def similarity(self, idxs):
+        """Score the (P, 2) pairs into Ds (base class: zeros, :121-140)."""
+        idxs = np.asarray(idxs)
+        for key in self.Ds:
+            self.Ds[key][idxs[:, 0], idxs[:, 1]] = 0.0
+
+    def all_pairwise(self, parallel=0, n_cores=12, symmetric=False, precomputed=False):
+        prefix = self.get_cacheprefix()
+        if precomputed:
+            self._load_Ds(prefix)
+            self.get_all_clique_ids()
+            return
+        self.prepare()
+        world, rank = _dist_info()
+        if world > 1:
+            bounds = _dist.stripe_bounds(self.track_lengths(), world, symmetric, m=0, tau=0)
+        else:
+            bounds = [(0, self.N)]
+        r0, r1 = bounds[rank]
+        pairs = _dist.stripe_pairs(self.N, r0, r1, symmetric)
+        for c0 in range(0, len(pairs), PAIR_CHUNK):
+            self.similarity(pairs[c0:c0 + PAIR_CHUNK])
+        if world > 1:
+            self._gather_stripes(bounds, r0, r1)
+        if symmetric:
+            for key in self.Ds:
+                self.Ds[key] += self.Ds[key].T
+        if rank == 0:
+            self._save_Ds(prefix)
+
+    def _gather_stripes(self, bounds, r0, r1):
+        import torch
+        dev = "cuda" if torch.cuda.is_available() else "cpu"
+        for key in self.Ds:
+            blk = torch.as_tensor(np.array(self.Ds[key][r0:r1])).to(dev)
+            full = _dist.all_gather_stripes(blk, bounds)
+            self.Ds[key][:] = full.cpu().numpy()
+
+    def _save_Ds(self, prefix):
+        np.savez("%s_Ds.npz" % prefix, **{k: np.asarray(v) for k, v in self.Ds.items()})
+
+    def _load_Ds(self, prefix):
+        npz, h5 = "%s_Ds.npz" % prefix, "%s_Ds.h5" % prefix
+        if os.path.exists(npz):
+            with np.load(npz, allow_pickle=False) as z:
+                self.Ds = {k: np.array(z[k]) for k in z.files}
+        else:
+            from ..features_io import _load_h5
+            self.Ds = _load_h5(h5)
+
+    def cleanup_memmap(self):
+        """Delete the memmap files of Ds (:195-203)."""
+        for s in list(self.Ds):
+            path = "%s_%s_dmat" % (self.get_cacheprefix(), s)
+            try:
+                if os.path.exists(path):
+                    os.remove(path)
+            except OSError:
+                print("Could not clean-up automatically.")
+
+    # ------------------------------------------------------------------ evaluation
+    def getEvalStatistics(self, similarity_type, topsidx=[1, 10, 100, 1000]):
+        """MR, MRR, MDR, MAP, Top-k of Ds[similarity_type] (:206-291); prints them and appends
+        a row to 'results_<shortname>_<name>.csv'."""
+        D = np.array(self.Ds[similarity_type], dtype=np.float32)
+        cliques = [sorted(self.cliques[s]) for s in self.cliques]
+        stats = evaluation.eval_statistics_cliques(D, cliques, topsidx)
+        MR, MRR, MDR, MAP, tops = stats
+        if np.isnan(MR):
+            warnings.warn("no clique with at least two songs")
+        print("%s %s STATS\n-------------------------\nMR = %.3g\nMRR = %.3g\nMDR = %.3g\nMAP = %.3g"
+              % (self.name, similarity_type, MR, MRR, MDR, MAP))
+        for t, v in zip(topsidx, tops):
+            print("Top-%i: %i" % (t, v))
+        evaluation.write_results_csv("results_%s_%s.csv" % (self.shortname, self.name), self.name, similarity_type,
+                                     stats, topsidx)
+        return MR, MRR, MDR, MAP, tops

@@ -1,0 +1,214 @@
+"""EarlyFusion — early MFCC/HPCP fusion (acoss/algorithms/earlyfusion_traile.py), MI355X engine.
+
+Tralie, C.J., 2017. Early mfcc and hpcp fusion for robust cover song identification.
+arXiv preprint arXiv:1707.04680.
+
+Per pair (A15, :157-198) everything runs on the GPU through the C-ABI: three CSMs on MFMA
+(euclidean on the MFCC blocks and on the SSM blocks, blocked-OTI cosine on the chroma
+blocks), kappa-NN binarisation, getWCSM of each CSM, their sum -> exp(-sum) -> binarisation,
+and the four constrained Smith-Waterman alignments of a chunk in one launch.
+
+The beat-synchronous block features (load_features, :67-154) are per-track preprocessing
+ and run on the host. They need skimage.transform.resize, which this
+image lacks: `resize_block` restates skimage >= 0.19 `resize(..., anti_aliasing=True,
+mode='constant')` (Gaussian pre-filter with sigma = max(0, (factor - 1) / 2), then a
+grid-mode linear zoom with zero fill) with scipy.ndimage. That restatement is unpinned.
+"""
+import argparse
+import os
+import time
+
+import numpy as np
+
+from .. import _lib
+from ..features_io import load_features as _load_feature_file
+from ..features_io import save_features as _save_feature_file
+from .algorithm_template import CoverAlgorithm
+from .utils.cross_recurrence import nneighbs
+from .utils.similarity_fusion import doSimilarityFusion
+
+__all__ = ["EarlyFusion", "resize_block"]
+
+
+def resize_block(X, i1, i2, frames_per_block, median_aggregate=False):
+    """Resample X[i1:i2] to frames_per_block rows (earlyfusion_traile.py:214-247)."""
+    from scipy import ndimage
+    if median_aggregate:
+        raise NotImplementedError("median_aggregate=True needs librosa.util.sync (absent); the reference default "
+                                  "is False")
+    x = np.asarray(X[i1:i2, :], dtype=np.float64)
+    factor = x.shape[0] / float(frames_per_block)
+    sigma = max(0.0, (factor - 1.0) / 2.0)
+    if sigma > 0:
+        x = ndimage.gaussian_filter(x, (sigma, 0.0), mode="constant", cval=0.0)
+    ret = ndimage.zoom(x, (frames_per_block / float(x.shape[0]), 1.0), order=1, mode="grid-constant", cval=0.0,
+                       grid_mode=True)
+    ret[np.isinf(ret)] = 0
+    ret[np.isnan(ret)] = 0
+    return ret
+
+
+def _ssm_upper(xn, I, J):
+    sq = np.sum(xn ** 2, 1)
+    D = sq[:, None] + sq[None, :] - 2 * xn.dot(xn.T)
+    D[D < 0] = 0
+    np.fill_diagonal(D, 0)
+    return np.sqrt(D)[I < J]
+
+
+class EarlyFusion(CoverAlgorithm):
+    def __init__(self, dataset_csv, datapath, chroma_type='hpcp', shortname='Covers80', blocksize=20,
+                 mfccs_per_block=50, ssm_res=50, chromas_per_block=40, kappa=0.1, K=10, niters=5, log_times=False,
+                 cachedir="cache"):
+        self.chroma_type = chroma_type
+        self.blocksize = blocksize
+        self.mfccs_per_block = mfccs_per_block
+        self.chromas_per_block = chromas_per_block
+        self.kappa = kappa
+        self.K = K
+        self.niters = niters
+        self.all_block_feats = {}
+        self.log_times = log_times
+        if log_times:
+            self.times = {'features': [], 'raw': []}
+        self._dev = {}
+        CoverAlgorithm.__init__(self, dataset_csv=dataset_csv, name="EarlyFusionTraile", datapath=datapath,
+                                shortname=shortname, similarity_types=["mfccs", "ssms", "chromas", "early"],
+                                cachedir=cachedir)
+
+    def get_cacheprefix(self):
+        return "%s/%s_%s_%s" % (self.cachedir, self.name, self.shortname, self.chroma_type)
+
+    def load_features(self, i, do_plot=False):
+        """Blocked features of song i: 'mfccs', 'ssms', 'chromas', 'chroma_med' (:67-154),
+        cached in memory and on disk ('<prefix>_<i>.npz')."""
+        filepath = "%s_%i.h5" % (self.get_cacheprefix(), i)
+        if i in self.all_block_feats:
+            return self.all_block_feats[i]
+        try:
+            self.all_block_feats[i] = _load_feature_file(filepath)
+            CoverAlgorithm.load_features(self, i)
+            return self.all_block_feats[i]
+        except IOError:
+            pass
+        tic = time.time()
+        feats = CoverAlgorithm.load_features(self, i)
+        chroma = np.asarray(feats[self.chroma_type])
+        mfcc = np.array(feats['mfcc_htk']).T
+        mfcc[np.isnan(mfcc)] = 0
+        onsets = np.asarray(feats['madmom_features']['onsets'])
+        n_blocks = len(onsets) - self.blocksize
+        bf = {}
+        bf['mfccs'] = np.zeros((n_blocks, self.mfccs_per_block * mfcc.shape[1]), dtype=np.float32)
+        pix = np.arange(self.mfccs_per_block)
+        I, J = np.meshgrid(pix, pix)
+        bf['ssms'] = np.zeros((n_blocks, int(self.mfccs_per_block * (self.mfccs_per_block - 1) / 2)),
+                              dtype=np.float32)
+        for b in range(n_blocks):
+            x = resize_block(mfcc, onsets[b], onsets[b + self.blocksize - 1], self.mfccs_per_block)
+            x -= np.mean(x, 0)[None, :]
+            xnorm = np.sqrt(np.sum(x ** 2, 1))[:, None]
+            xnorm[xnorm == 0] = 1
+            xn = x / xnorm
+            bf['mfccs'][b, :] = xn.flatten()
+            bf['ssms'][b, :] = _ssm_upper(xn, I, J)
+        bf['chromas'] = np.zeros((n_blocks, self.chromas_per_block * chroma.shape[1]), dtype=np.float32)
+        bf['chroma_med'] = np.median(chroma, axis=0)
+        for b in range(n_blocks):
+            x = resize_block(chroma, onsets[b], onsets[b + self.blocksize], self.chromas_per_block)
+            bf['chromas'][b, :] = x.flatten()
+        self.all_block_feats[i] = bf
+        _save_feature_file(filepath, bf)
+        if self.log_times:
+            self.times['features'].append(time.time() - tic)
+        return bf
+
+    def _device(self, i):
+        if i not in self._dev:
+            torch = _lib._torch()
+            f = self.load_features(i)
+            self._dev[i] = {k: torch.as_tensor(np.ascontiguousarray(f[k], np.float32)).cuda()
+                            for k in ("mfccs", "ssms", "chromas")}
+            self._dev[i]["chroma_med"] = np.asarray(f["chroma_med"], np.float32)
+        return self._dev[i]
+
+    def pair_matrices(self, i, j):
+        """The four binary matrices of pair (i, j) (device uint8), in score order
+        mfccs, ssms, chromas, early (:157-189)."""
+        torch = _lib._torch()
+        a, b = self._device(i), self._device(j)
+        csms = {}
+        csms['mfccs'] = _lib.csm(a['mfccs'], b['mfccs'], kind="euclidean")
+        csms['ssms'] = _lib.csm(a['ssms'], b['ssms'], kind="euclidean")
+        oti = int(_lib.get_oti(a['chroma_med'], b['chroma_med']).item())
+        csms['chromas'] = _lib.csm(a['chromas'], b['chromas'], kind="cosine", oti_shift=oti)
+        ncols = csms['mfccs'].shape[1]
+        nn = nneighbs(self.kappa, ncols)
+        mats = [_lib.binarize_rows(csms[s], nn) for s in ('mfccs', 'ssms', 'chromas')]
+        wsum = torch.zeros_like(csms['mfccs'])
+        for s in ('mfccs', 'ssms', 'chromas'):
+            wsum += _lib.wcsm(csms[s], self.K, self.K, 0.5)
+        mats.append(_lib.binarize_rows(torch.exp(-wsum), nn))
+        return mats
+
+    def similarity(self, idxs, do_plot=False):
+        idxs = np.asarray(idxs)
+        if len(idxs) == 0:
+            return
+        keys = ("mfccs", "ssms", "chromas", "early")
+        step = 512
+        for c0 in range(0, len(idxs), step):
+            chunk = idxs[c0:c0 + step]
+            tic = time.time()
+            mats = []
+            for i, j in chunk:
+                mats.extend(self.pair_matrices(int(i), int(j)))
+            scores = _lib.sw_constrained(mats).cpu().numpy().reshape(len(chunk), 4)
+            if self.log_times:
+                self.times['raw'].append((time.time() - tic) / len(chunk))
+            for s, key in enumerate(keys):
+                self.Ds[key][chunk[:, 0], chunk[:, 1]] = scores[:, s]
+
+    def prepare(self):
+        if not self._prepared:
+            for i in range(self.N):
+                self.load_features(i)
+            self._prepared = True
+
+    def do_late_fusion(self):
+        """SNF of 1/(1 + D) for the late and early+late outputs (:200-206)."""
+        self.Ds["late"] = doSimilarityFusion([1.0 / (1.0 + self.Ds[s]) for s in ["chromas", "ssms", "mfccs"]], K=20,
+                                             niters=20, reg_diag=1)[1]
+        self.Ds["early+late"] = doSimilarityFusion([1.0 / (1.0 + self.Ds[s])
+                                                    for s in ["chromas", "ssms", "mfccs", "early"]], K=20, niters=20,
+                                                   reg_diag=1)[1]
+
+
+if __name__ == '__main__':
+    parser = argparse.ArgumentParser(description="Benchmarking with Early Similarity Network Fusion of HPCP, MFCC, "
+                                                 "and MFCC SSMs",
+                                     formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    parser.add_argument("-i", '--dataset_csv', type=str, action="store", help="Input dataset csv file")
+    parser.add_argument("-d", '--datapath', type=str, action="store", default='../features_covers80',
+                        help="Path to data files")
+    parser.add_argument("-s", "--shortname", type=str, action="store", default="Covers80", help="Short name for dataset")
+    parser.add_argument("-c", '--chroma_type', type=str, action="store", default='hpcp',
+                        help="Type of chroma to use for experiments")
+    parser.add_argument("-p", '--parallel', type=int, choices=(0, 1), action="store", default=0, help="Ignored")
+    parser.add_argument("-n", '--n_cores', type=int, action="store", default=1, help="Ignored")
+    parser.add_argument("-l", '--log_times', type=int, choices=(0, 1), action="store", default=0,
+                        help="Whether to log times to a file")
+    cmd_args = parser.parse_args()
+    ef = EarlyFusion(dataset_csv=cmd_args.dataset_csv, datapath=cmd_args.datapath, chroma_type=cmd_args.chroma_type,
+                     shortname=cmd_args.shortname, log_times=bool(cmd_args.log_times))
+    for i in range(len(ef.filepaths)):
+        ef.load_features(i)
+    ef.all_pairwise(cmd_args.parallel, cmd_args.n_cores, symmetric=True)
+    ef.do_late_fusion()
+    for similarity_type in ef.Ds:
+        ef.getEvalStatistics(similarity_type)
+    ef.cleanup_memmap()
+    if ef.log_times:
+        for s in ef.times:
+            print("%s: %.3g" % (s, np.mean(ef.times[s])))
+    print("... Done ....")

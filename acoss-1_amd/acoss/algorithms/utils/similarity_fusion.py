@@ -1,0 +1,178 @@
+"""Similarity network fusion (acoss/algorithms/utils/similarity_fusion.py) on the GPU.
+
+Same functions and arguments as the reference; numpy in, numpy out, device tensors inside.
+`getWCSM` runs the HIP kernel (misc.hip); the N x N fusion runs as device tensor ops: the
+kNN sets come from torch.topk, and the sparse S . P . S^T products are row gathers
+(S holds K entries per row), so an iteration is O(N^2 K), not a dense N^3 GEMM.
+
+Two reference behaviours are kept on purpose:
+  * dtypes follow numpy's: float32 inputs give float32 W/P, the diffusion runs in float64;
+  * in doSimilarityFusionWs, `Pts = nextPts` aliases the two lists after the first
+    iteration, so from the second iteration on every update of matrix i already sees the
+    updated matrices k < i (similarity_fusion.py:157-177). The loop below is written the
+    same way, so it has the same aliasing.
+The kNN choices among exactly tied values are unspecified in both (np.argpartition / topk).
+"""
+import numpy as np
+
+from ... import _lib
+
+__all__ = ["getW", "getWCSM", "setupWCSMSSM", "getWCSMSSM", "getP", "getS", "doSimilarityFusionWs",
+           "doSimilarityFusion"]
+
+
+def _t(x, dtype=None):
+    torch = _lib._torch()
+    if isinstance(x, torch.Tensor):
+        t = x.cuda()
+    else:
+        a = np.asarray(x)
+        t = torch.as_tensor(np.ascontiguousarray(a)).cuda()
+    return t.to(dtype) if dtype is not None else t
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _getW(D, K, Mu=0.5):
+    torch = _lib._torch()
+    DSym = 0.5 * (D + D.T)
+    DSym.fill_diagonal_(0)
+    Neighbs = torch.topk(DSym, K + 1, dim=1, largest=False).values
+    MeanDist = Neighbs.mean(1) * (float(K + 1) / float(K))
+    Eps = (MeanDist[:, None] + MeanDist[None, :] + DSym) / 3
+    Denom = 2 * (Mu * Eps) ** 2
+    Denom[Denom == 0] = 1
+    return torch.exp(-DSym ** 2 / Denom)
+
+
+def getW(D, K, Mu=0.5):
+    """Affinity matrix (similarity_fusion.py:15-36)."""
+    return _np(_getW(_t(D), K, Mu))
+
+
+def getWCSM(CSMAB, k1, k2, Mu=0.5):
+    """Cross-similarity affinity (similarity_fusion.py:38-54), HIP kernel."""
+    return _np(_lib.wcsm(np.asarray(CSMAB, np.float32), k1, k2, Mu))
+
+
+def setupWCSMSSM(WSSMA, WSSMB, WCSMAB):
+    """[[WSSMA, WCSMAB], [WCSMAB^T, WSSMB]] (similarity_fusion.py:56-74)."""
+    M, N = WSSMA.shape[0], WSSMB.shape[0]
+    W = np.zeros((N + M, N + M))
+    W[:M, :M] = WSSMA
+    W[:M, M:] = WCSMAB
+    W[M:, :M] = WCSMAB.T
+    W[M:, M:] = WSSMB
+    return W
+
+
+def getWCSMSSM(SSMA, SSMB, CSMAB, K, Mu=0.5):
+    """Parent W with the neighbours split between SSM and CSM parts (similarity_fusion.py:76-96)."""
+    M, N = SSMA.shape[0], SSMB.shape[0]
+    k1 = int(K * float(M) / (M + N))
+    k2 = K - k1
+    return setupWCSMSSM(getW(SSMA, k1, Mu), getW(SSMB, k2, Mu), getWCSM(CSMAB, k1, k2, Mu))
+
+
+def _getP(W, diagRegularize=False):
+    torch = _lib._torch()
+    if diagRegularize:
+        WNoDiag = W.clone()
+        WNoDiag.fill_diagonal_(0)
+        RowSum = WNoDiag.sum(1)
+        RowSum[RowSum == 0] = 1
+        eye = torch.eye(W.shape[0], dtype=torch.float64, device=W.device)
+        return 0.5 * eye + 0.5 * WNoDiag / RowSum[:, None]
+    RowSum = W.sum(1)
+    RowSum[RowSum == 0] = 1
+    return W / RowSum[:, None]
+
+
+def getP(W, diagRegularize=False):
+    """Row-normalised probability matrix (similarity_fusion.py:98-119)."""
+    return _np(_getP(_t(W), diagRegularize))
+
+
+class _KNN:
+    """Row-sparse matrix with K entries per row: S[i, J[i, k]] = V[i, k]."""
+
+    def __init__(self, J, V, n):
+        self.J, self.V, self.n = J, V, n
+
+    def dot(self, X, chunk_bytes=1 << 29):
+        """S . X for dense X (n x m), in float64 like scipy's csr(float32) . ndarray(float64)."""
+        torch = _lib._torch()
+        X = X.to(torch.float64)
+        out = torch.empty((self.n, X.shape[1]), dtype=torch.float64, device=X.device)
+        K = self.J.shape[1]
+        rows = max(1, int(chunk_bytes // max(1, K * X.shape[1] * 8)))
+        Vd = self.V.to(torch.float64)
+        for r0 in range(0, self.n, rows):
+            r1 = min(self.n, r0 + rows)
+            g = X[self.J[r0:r1].reshape(-1)].reshape(r1 - r0, K, X.shape[1])
+            out[r0:r1] = torch.einsum("rk,rkm->rm", Vd[r0:r1], g)
+        return out
+
+    def todense(self):
+        torch = _lib._torch()
+        S = torch.zeros((self.n, self.n), dtype=self.V.dtype, device=self.V.device)
+        S.scatter_(1, self.J, self.V)
+        return S
+
+
+def _getS(W, K):
+    torch = _lib._torch()
+    V, J = torch.topk(W, K, dim=1, largest=True)
+    SNorm = V.sum(1)
+    SNorm[SNorm == 0] = 1
+    return _KNN(J, V / SNorm[:, None], W.shape[0])
+
+
+def getS(W, K):
+    """kNN-truncated, row-normalised W (similarity_fusion.py:121-143), as a scipy CSR matrix."""
+    from scipy import sparse
+    S = _getS(_t(W), K)
+    J, V = _np(S.J), _np(S.V)
+    n = W.shape[0]
+    return sparse.coo_matrix((V.ravel(), (np.repeat(np.arange(n), J.shape[1]), J.ravel())), shape=(n, n)).tocsr()
+
+
+def _fusion_ws(Ws, K=5, niters=20, reg_diag=1):
+    torch = _lib._torch()
+    Ps = [_getP(W) for W in Ws]
+    Ss = [_getS(W, K) for W in Ws]
+    Pts = [P.clone() for P in Ps]
+    nextPts = [torch.zeros(P.shape, dtype=torch.float64, device=P.device) for P in Pts]
+    N = len(Pts)
+    pix = torch.arange(Ws[0].shape[0], device=Ws[0].device)
+    for it in range(niters):
+        for i in range(N):
+            nextPts[i] *= 0
+            for k in range(N):
+                if i == k:
+                    continue
+                nextPts[i] += Pts[k]
+            nextPts[i] /= float(N - 1)
+            # S . P . S^T as in the reference: S.dot((S.dot(P.T)).T)
+            nextPts[i] = Ss[i].dot(Ss[i].dot(nextPts[i].T).T)
+            if reg_diag > 0:
+                nextPts[i][pix, pix] += reg_diag
+        Pts = nextPts
+    Fused = torch.zeros(Pts[0].shape, dtype=torch.float64, device=Pts[0].device)
+    for Pt in Pts:
+        Fused += Pt
+    return Fused / N
+
+
+def doSimilarityFusionWs(Ws, K=5, niters=20, reg_diag=1):
+    """Cross-diffusion of affinity matrices (similarity_fusion.py:145-182)."""
+    return _np(_fusion_ws([_t(W) for W in Ws], K, niters, reg_diag))
+
+
+def doSimilarityFusion(Scores, K=5, niters=5, reg_diag=1):
+    """(list of W, fused similarity) from N x N distance matrices (similarity_fusion.py:184-192)."""
+    Ws = [_getW(_t(D), K) for D in Scores]
+    fused = _fusion_ws(Ws, K, niters, reg_diag)
+    return [_np(W) for W in Ws], _np(fused)

@@ -22,15 +22,23 @@ def stacked_len(n, m=9, tau=1):
 class ChromaBank:
     """12-bin chroma of a whole corpus resident on the current GPU."""
 
-    def __init__(self, tracks):
+    def __init__(self, tracks=None, packed=None):
+        """tracks: list of (n_i, 12) arrays, or packed=(feats (sum n, 12) f32 device tensor,
+        frame offsets, lengths) already resident in HBM."""
         torch = _lib._torch()
-        feats, off, lens = pack([np.asarray(t, np.float32) for t in tracks])
-        self.n_tracks = len(tracks)
-        self.lens = lens
-        self.max_len = int(lens.max()) if len(lens) else 0
-        self.feats = torch.as_tensor(feats).cuda()
-        self.off = torch.as_tensor(off).cuda()
-        self.len = torch.as_tensor(lens).cuda()
+        if packed is not None:
+            feats, off, lens = packed
+            self.lens = np.asarray(lens, np.int32)
+            self.feats = feats
+            self.off = torch.as_tensor(np.asarray(off, np.int64)).cuda()
+        else:
+            feats, off, lens = pack([np.asarray(t, np.float32) for t in tracks])
+            self.lens = lens
+            self.feats = torch.as_tensor(feats).cuda()
+            self.off = torch.as_tensor(off).cuda()
+        self.n_tracks = len(self.lens)
+        self.max_len = int(self.lens.max()) if len(self.lens) else 0
+        self.len = torch.as_tensor(self.lens).cuda()
 
     def crp_align(self, pairs, m=9, tau=1, kappa=0.095, oti=True, gamma_open=0.5, gamma_ext=0.5, qmax=True,
                   dmax=False, want_oti=False):

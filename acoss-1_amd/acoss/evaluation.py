@@ -30,13 +30,30 @@ def clique_order(labels):
 
 
 def eval_statistics(D, labels, topsidx=(1, 10, 100, 1000)):
-    """Return (MR, MRR, MDR, MAP, tops) exactly as getEvalStatistics computes them."""
+    """Return (MR, MRR, MDR, MAP, tops) exactly as getEvalStatistics computes them, with the
+    cliques given as one label per song (cliques ordered by first appearance)."""
+    perm, Ks = clique_order(labels)
+    cliques, start = [], 0
+    for K in Ks:
+        cliques.append(perm[start:start + K].tolist())
+        start += K
+    return eval_statistics_cliques(D, cliques, topsidx, presorted=True)
+
+
+def eval_statistics_cliques(D, cliques, topsidx=(1, 10, 100, 1000), presorted=False):
+    """getEvalStatistics on explicit cliques (lists of song indices, in the order of the
+    reference's `self.cliques` dict). Cliques are stably sorted by decreasing size (:219-225)
+    unless `presorted`."""
     D = np.array(D, dtype=np.float32)
     N = D.shape[0]
-    perm, Ks = clique_order(labels)
+    Ks = np.array([len(c) for c in cliques], dtype=np.int64)
+    if not presorted:
+        order = np.argsort(-Ks, kind="stable")
+        cliques = [cliques[i] for i in order]
+        Ks = Ks[order]
+    perm = np.array([i for c in cliques for i in c], dtype=np.int64)
     D = D[perm][:, perm]
     np.fill_diagonal(D, -np.inf)
-    lab = np.repeat(np.arange(len(Ks)), Ks)
     ranks = np.full(N, np.nan)
     allmap = np.full(N, np.nan)
     # row-wise descending order, stable (index order breaks ties)
@@ -45,7 +62,7 @@ def eval_statistics(D, labels, topsidx=(1, 10, 100, 1000)):
     rows = np.arange(N)[:, None]
     pos[rows, order] = np.arange(N)[None, :]
     start = 0
-    for c, K in enumerate(Ks):
+    for K in Ks:
         if K < 2:
             break
         members = np.arange(start, start + K)

@@ -1,0 +1,87 @@
+"""Per-track feature files: the dict the reference reads with deepdish (`dd.io.load`,
+acoss/algorithms/algorithm_template.py:90; written by acoss/extractors.py:114).
+
+Keys (README.md:93-114): 'hpcp', 'crema', 'chroma_cens' (n, 12) float32, 'mfcc_htk'
+(n_coeffs, n), 'madmom_features' {'onsets': int64, ...}, 'label', 'track_id', ...
+
+Readers, in order:
+  1. `<path>` itself when it is HDF5 and h5py is importable (deepdish's layout: datasets for
+     arrays, groups for nested dicts, scalar/str datasets or attributes for the rest);
+  2. the same path with the suffix `.npz` (np.load, allow_pickle=False), nested keys
+     flattened as 'madmom_features/onsets'. This image has neither h5py nor PyTables, so the
+     tests and the synthetic datasets use this form (`save_features`).
+"""
+import os
+
+import numpy as np
+
+
+def _npz_path(path):
+    root, ext = os.path.splitext(path)
+    return root + ".npz" if ext != ".npz" else path
+
+
+def _unflatten(flat):
+    out = {}
+    for key, val in flat.items():
+        parts = key.split("/")
+        d = out
+        for p in parts[:-1]:
+            d = d.setdefault(p, {})
+        if isinstance(val, np.ndarray) and val.ndim == 0:
+            val = val.item()
+        d[parts[-1]] = val
+    return out
+
+
+def _flatten(feats, prefix=""):
+    flat = {}
+    for k, v in feats.items():
+        name = prefix + str(k)
+        if isinstance(v, dict):
+            flat.update(_flatten(v, name + "/"))
+        else:
+            flat[name] = np.asarray(v)
+    return flat
+
+
+def _load_h5(path):
+    import h5py  # optional
+
+    def walk(g):
+        d = {}
+        for k, v in g.items():
+            if isinstance(v, h5py.Group):
+                d[k] = walk(v)
+            else:
+                a = v[()]
+                d[k] = a.decode() if isinstance(a, bytes) else a
+        for k, v in g.attrs.items():
+            if k not in d and not k.startswith("DEEPDISH") and not k.startswith("CLASS"):
+                d[k] = v.decode() if isinstance(v, bytes) else v
+        return d
+
+    with h5py.File(path, "r") as f:
+        return walk(f)
+
+
+def load_features(path):
+    """Feature dict of one track; IOError if no readable file exists."""
+    if os.path.exists(path) and not path.endswith(".npz"):
+        try:
+            return _load_h5(path)
+        except ImportError:
+            pass
+    p = _npz_path(path)
+    if os.path.exists(p):
+        with np.load(p, allow_pickle=False) as z:
+            return _unflatten({k: z[k] for k in z.files})
+    raise IOError("no readable feature file for %s (looked for HDF5 with h5py, and %s)" % (path, p))
+
+
+def save_features(path, feats):
+    """Write `feats` as the .npz twin of `path` (creates the directory)."""
+    p = _npz_path(path)
+    os.makedirs(os.path.dirname(p) or ".", exist_ok=True)
+    np.savez(p, **_flatten(feats))
+    return p

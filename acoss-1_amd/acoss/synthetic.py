@@ -100,3 +100,32 @@ def pack(tracks):
         off[1:] = np.cumsum(lens[:-1])
     feats = np.ascontiguousarray(np.concatenate(tracks, 0), np.float32) if tracks else np.zeros((0, 12), np.float32)
     return feats, off, lens
+
+
+def write_feature_dataset(root, tracks, labels, with_mfcc=False, seed=SEED, beat_period=43):
+    """Write a dataset the plugin classes can read: '<root>/dataset.csv' (work_id, track_id)
+    and one feature file per track at '<root>/features/<work_id>/<track_id>.npz' with the keys
+    of the reference's feature dicts (README.md:93-114): 'hpcp', 'crema', 'chroma_cens',
+    'label', 'track_id', and with_mfcc: 'mfcc_htk' (20, n) and 'madmom_features/onsets'
+    (a fixed beat grid with jitter). Returns (csv path, feature dir with trailing slash)."""
+    from .features_io import save_features
+    rng = np.random.Generator(np.random.PCG64(seed))
+    feat_dir = os.path.join(root, "features") + "/"
+    rows = []
+    for k, (t, lab) in enumerate(zip(tracks, labels)):
+        work, track = "W%05d" % int(lab), "T%06d" % k
+        t = np.asarray(t, np.float32)
+        f = {"hpcp": t, "crema": t, "chroma_cens": t, "label": work, "track_id": track}
+        if with_mfcc:
+            n = len(t)
+            f["mfcc_htk"] = rng.standard_normal((20, n)).astype(np.float32)
+            beats = np.arange(0, n - 1, beat_period) + rng.integers(0, 3, size=len(range(0, n - 1, beat_period)))
+            f["madmom_features"] = {"onsets": np.unique(np.clip(beats, 0, n - 1)).astype(np.int64)}
+        save_features(feat_dir + work + "/" + track + ".h5", f)
+        rows.append((work, track))
+    csv = os.path.join(root, "dataset.csv")
+    with open(csv, "w") as fo:
+        fo.write("work_id,track_id\n")
+        for w, tr in rows:
+            fo.write("%s,%s\n" % (w, tr))
+    return csv, feat_dir

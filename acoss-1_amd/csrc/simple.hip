@@ -59,7 +59,7 @@ __global__ void k_simple_track(const double* __restrict__ feats, const int64_t* 
 __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ feats, const int64_t* __restrict__ off,
                                                      const int32_t* __restrict__ len, const int32_t* __restrict__ pairs,
                                                      const double* __restrict__ prof, const double* __restrict__ fnorm,
-                                                     int64_t ldf, int L, double* __restrict__ score,
+                                                     int64_t ldf, int L, int apply_oti, double* __restrict__ score,
                                                      int32_t* __restrict__ oti_out) {
   __shared__ double sa[kMaxLen];
   __shared__ double sb[kMaxLen];
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ 
         best = k;
       }
     }
-    s_k = best;
+    s_k = apply_oti ? best : 0;
     if (oti_out) oti_out[p] = best;
   }
   if (P <= 0 || Q <= 0) {
@@ -178,7 +178,7 @@ using namespace acoss;
 
 extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, const int32_t* track_len,
                                int32_t n_tracks, int32_t max_len, const int32_t* pairs, int64_t n_pairs, int32_t sslen,
-                               double* score_out, int32_t* oti_out, void* hip_stream) {
+                               int32_t apply_oti, double* score_out, int32_t* oti_out, void* hip_stream) {
   clear_error();
   if (n_tracks < 0 || n_pairs < 0 || (n_pairs > 0 && (!feats || !track_off || !track_len || !pairs || !score_out))) {
     set_error("acoss_simple_mp: bad arguments");
@@ -207,7 +207,7 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
   for (int64_t p0 = 0; p0 < n_pairs; p0 += 1 << 20) {
     const int64_t np = std::min<int64_t>(n_pairs - p0, 1 << 20);
     hipLaunchKernelGGL(k_simple_pair, dim3((unsigned)np), dim3(256), 0, s, feats, track_off, track_len, pairs + 2 * p0,
-                       prof, fnorm, ldf, sslen, score_out + p0, oti_out ? oti_out + p0 : nullptr);
+                       prof, fnorm, ldf, sslen, apply_oti, score_out + p0, oti_out ? oti_out + p0 : nullptr);
     ACOSS_LAUNCH_CHECK();
   }
   prof_end(PH_SIMPLE, s);

@@ -121,10 +121,30 @@ int acoss_wcsm(const float* CSM, int32_t M, int32_t N, int32_t k1, int32_t k2, f
  * ordered pairs, including the per-pair OTI roll of the reference (Simple.oti, :45-54).
  * feats: packed (12 x n_t) float64 blocks, track t at element offset track_off[t] (dim-major,
  * as the reference's seq arrays). score_out[p] = median_i min_j dist (the reference stores
- * -score, simple_silva.py:125). oti_out may be NULL. */
+ * -score, simple_silva.py:125). apply_oti = 0 scores the reference as given (Simple.simple_sim
+ * alone); oti_out (may be NULL) always receives the Simple.oti index. */
 int acoss_simple_mp(const double* feats, const int64_t* track_off, const int32_t* track_len, int32_t n_tracks,
-                    int32_t max_len, const int32_t* pairs, int64_t n_pairs, int32_t sslen, double* score_out,
-                    int32_t* oti_out, void* hip_stream);
+                    int32_t max_len, const int32_t* pairs, int64_t n_pairs, int32_t sslen, int32_t apply_oti,
+                    double* score_out, int32_t* oti_out, void* hip_stream);
+
+/* Per-track median downsampling of chroma (A13: Serra09/ChenFusion.load_features,
+ * acoss/algorithms/rqa_serra09.py:44-53 and latefusion_chen.py:46-56, which call
+ * librosa.util.sync(chroma.T, arange(0, n, factor), aggregate=np.median)).
+ * feats: packed (sum n, 12) float32, track t at frame offset track_off[t]; max_len = max n.
+ * out: track t's ceil(n_t / factor) x 12 float32 rows at frame offset out_off[t].
+ * factor <= 64. */
+int acoss_median_downsample(const float* feats, const int64_t* track_off, const int32_t* track_len, int32_t n_tracks,
+                            int32_t max_len, int32_t factor, float* out, const int64_t* out_off, void* hip_stream);
+
+/* Per-track SiMPle features (A12: Simple.load_features + Simple.smooth,
+ * acoss/algorithms/simple_silva.py:34-43,56-66): window means (win=200, hop skip=100) ->
+ * 'same' zero-filled convolution with the host weights smooth[0..smooth_len) (normalised
+ * symmetric Hann(6) in the reference) -> per-column L2 normalisation.
+ * out: track t's (12 x floor(n_t / skip)) float64 block (dim-major) at element offset
+ * out_off[t]; out_elems = total doubles in out. smooth is a HOST pointer. */
+int acoss_simple_features(const float* feats, const int64_t* track_off, const int32_t* track_len, int32_t n_tracks,
+                          int32_t win, int32_t skip, const double* smooth, int32_t smooth_len, double* out,
+                          const int64_t* out_off, int64_t out_elems, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,154 @@
+"""GPU tests of the plugin layer: feature-prep kernels, SNF, and end-to-end
+coverid.benchmark runs on synthetic on-disk datasets, each checked against the oracle.
+
+Bars: median downsample bit-exact (same float32 arithmetic as np.median); SiMPle features
+within 1e-12 relative of the numpy restatement (convolution order); Serra09/Chen Ds
+bit-exact vs oracle.crp_batch on the oracle's own features, after the reference's
+symmetrisation and length normalisation; SiMPle Ds bit-exact vs the C oracle on the GPU's
+features; SNF within 1e-9 of the reference's golden output; EarlyFusion's composition
+checked per stage (CSM tolerance, SW exact on the produced binary matrices)."""
+import numpy as np
+import pytest
+
+import oracle
+from oracle import np_oracle as npo
+from acoss import _lib, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gold():
+    from conftest import GOLDEN
+    return np.load(GOLDEN)
+
+
+def _tracks(lengths, seed=3):
+    rng = np.random.default_rng(seed)
+    return [np.abs(rng.standard_normal((n, 12))).astype(np.float32) for n in lengths]
+
+
+def test_median_downsample_bitexact():
+    tr = _tracks([1, 39, 40, 41, 80, 1999, 2000, 2401])
+    tr[3][5:9] = 0.25  # ties inside a segment
+    feats, off, lens = synthetic.pack(tr)
+    out, out_off, out_len = _lib.median_downsample(feats, off, lens, 40)
+    host = out.cpu().numpy()
+    for t, o, n in zip(tr, out_off, out_len):
+        np.testing.assert_array_equal(host[o:o + n], npo.median_downsample(t, 40))
+
+
+def test_simple_features_match_restatement():
+    tr = _tracks([100, 250, 2000, 2099, 5123])
+    feats, off, lens = synthetic.pack(tr)
+    out, out_off, T = _lib.simple_features(feats, off, lens)
+    host = out.cpu().numpy()
+    for t, o, n in zip(tr, out_off, T):
+        ref = npo.simple_features(t)
+        got = host[o:o + 12 * n].reshape(12, n)
+        np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-15)
+
+
+def test_snf_golden(gold):
+    from acoss.algorithms.utils.similarity_fusion import doSimilarityFusion
+    Ws, fused = doSimilarityFusion(list(gold["snf_D"]), K=5, niters=5, reg_diag=1)
+    np.testing.assert_allclose(fused, gold["snf_fused"], rtol=1e-9, atol=1e-12)
+
+
+def _dataset(tmp_path, frames=2400, mfcc=False, n_cliques=None):
+    tracks, labels = synthetic.make_corpus("covers80", frames=frames, seed=11)
+    keep = np.flatnonzero(labels < (n_cliques or 8))
+    tracks = [tracks[k] for k in keep]
+    labels = labels[keep]
+    csv, fdir = synthetic.write_feature_dataset(str(tmp_path), tracks, labels, with_mfcc=mfcc)
+    return csv, fdir, tracks, labels
+
+
+def _oracle_crp_D(tracks, dmax=False):
+    ds = [npo.median_downsample(t, 40) for t in tracks]
+    feats, off, lens = synthetic.pack(ds)
+    n = len(ds)
+    pairs = np.array([(i, j) for i in range(n) for j in range(i + 1, n)], np.int32)
+    q, d, _ = oracle.crp_batch(feats, off, lens, pairs, dmax=dmax)
+    out = []
+    for v in ([q, d] if dmax else [q]):
+        D = np.zeros((n, n), np.float32)
+        D[pairs[:, 0], pairs[:, 1]] = v
+        D += D.T
+        out.append(D)
+    return out, np.array([len(x) for x in ds])
+
+
+def test_benchmark_serra09_matches_oracle(tmp_path, monkeypatch):
+    from acoss import coverid, evaluation
+    monkeypatch.chdir(tmp_path)
+    csv, fdir, tracks, labels = _dataset(tmp_path)
+    algo = coverid.benchmark(csv, fdir, algorithm="Serra09", shortname="t", cachedir=str(tmp_path / "cache"))
+    (D,), lens = _oracle_crp_D(tracks)
+    D = (D / np.sqrt(lens.astype(np.float64))[None, :]).astype(np.float32)
+    got = np.asarray(algo.Ds["main"])
+    np.testing.assert_array_equal(got, D)
+    ref_stats = evaluation.eval_statistics(D, labels)
+    assert algo.getEvalStatistics("main")[3] == ref_stats[3]
+
+
+def test_benchmark_chen_matches_oracle(tmp_path, monkeypatch):
+    from acoss.algorithms.latefusion_chen import ChenFusion
+    monkeypatch.chdir(tmp_path)
+    csv, fdir, tracks, labels = _dataset(tmp_path, n_cliques=12)  # SNF K=20 needs > 21 songs
+    a = ChenFusion(csv, fdir, shortname="t", cachedir=str(tmp_path / "cache"))
+    a.all_pairwise(symmetric=True)
+    (Q, Dm), lens = _oracle_crp_D(tracks, dmax=True)
+    np.testing.assert_array_equal(np.asarray(a.Ds["qmax"]), Q)
+    np.testing.assert_array_equal(np.asarray(a.Ds["dmax"]), Dm)
+    with np.errstate(divide="ignore"):
+        a.normalize_by_length()
+        norm = np.sqrt(lens.astype(np.float64))[None, :]
+        np.testing.assert_array_equal(np.asarray(a.Ds["qmax"]), (norm / Q).astype(np.float32))
+    # late fusion needs finite inputs: replace the inf diagonal as a user of the fused output would see it
+    for k in a.Ds:
+        M = np.asarray(a.Ds[k])
+        M[~np.isfinite(M)] = 1e6
+        a.Ds[k][:] = M
+    a.do_late_fusion()
+    assert np.all(np.isfinite(a.Ds["Late"]))
+
+
+def test_benchmark_simple_matches_oracle(tmp_path, monkeypatch):
+    from acoss import coverid
+    monkeypatch.chdir(tmp_path)
+    csv, fdir, tracks, labels = _dataset(tmp_path, frames=3000, n_cliques=5)
+    algo = coverid.benchmark(csv, fdir, algorithm="SiMPle", shortname="t", cachedir=str(tmp_path / "cache"))
+    # the GPU's own features (bit-identical input) through the C oracle
+    feats = [algo.all_feats[i] for i in range(algo.N)]
+    n = len(feats)
+    D = np.zeros((n, n), np.float32)
+    for i in range(n):
+        np.testing.assert_allclose(feats[i], npo.simple_features(tracks[i]), rtol=1e-12, atol=1e-15)
+        for j in range(n):
+            if i != j:
+                k = oracle.simple_oti(feats[i], feats[j])
+                D[i, j] = -oracle.simple_sim(feats[i], np.roll(feats[j], k, axis=0))
+    np.testing.assert_array_equal(np.asarray(algo.Ds["main"]), D)
+
+
+def test_earlyfusion_composition(tmp_path, monkeypatch):
+    from acoss.algorithms.earlyfusion_traile import EarlyFusion
+    monkeypatch.chdir(tmp_path)
+    csv, fdir, tracks, labels = _dataset(tmp_path, frames=3000, mfcc=True, n_cliques=12)
+    ef = EarlyFusion(csv, fdir, shortname="t", cachedir=str(tmp_path / "cache"))
+    ef.all_pairwise(symmetric=True)
+    for (i, j) in [(0, 1), (1, 4), (2, 3)]:
+        f1, f2 = ef.load_features(i), ef.load_features(j)
+        mats = [m.cpu().numpy() for m in ef.pair_matrices(i, j)]
+        C = npo.get_csm(f1["mfccs"], f2["mfccs"])
+        B = npo.csm_to_binary(C, ef.kappa)
+        assert np.mean(B != mats[0]) < 0.01
+        Cc = npo.get_csm_blocked_oti(f1["chromas"], f2["chromas"], f1["chroma_med"], f2["chroma_med"],
+                                     npo.get_csm_cosine)
+        assert np.mean(npo.csm_to_binary(Cc, ef.kappa) != mats[2]) < 0.01
+        for s, key in enumerate(["mfccs", "ssms", "chromas", "early"]):
+            ref = oracle.sw_constrained(mats[s])
+            assert ef.Ds[key][i, j] == np.float32(ref)  # Ds is float32, like the memmap
+    ef.do_late_fusion()
+    assert np.all(np.isfinite(ef.Ds["late"])) and np.all(np.isfinite(ef.Ds["early+late"]))

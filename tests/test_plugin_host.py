@@ -1,0 +1,135 @@
+"""CPU tests of the plugin layer's host logic (no GPU): dataset CSV paths, feature files,
+the CoverAlgorithm pair driver (enumeration order, symmetrisation, persistence, evaluation)
+and its multi-rank path over gloo (world 2 must equal world 1 bitwise)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from acoss import features_io, synthetic, utils
+from acoss.algorithms.algorithm_template import CoverAlgorithm
+
+
+def test_create_dataset_filepaths(tmp_path):
+    csv = tmp_path / "d.csv"
+    csv.write_text("work_id,track_id\nW1,T1\nW1,T2\nW2,T3\n")
+    assert utils.create_dataset_filepaths(str(csv), "root/", ".h5") == ["root/W1/T1.h5", "root/W1/T2.h5",
+                                                                         "root/W2/T3.h5"]
+    bad = tmp_path / "b.csv"
+    bad.write_text("work,track_id\nW1,T1\n")
+    with pytest.raises(IOError):
+        utils.create_dataset_filepaths(str(bad), "root/")
+    assert len(utils.create_dataset_filepaths(utils.COVERS_80_CSV, "x/")) == 164
+    assert len(utils.create_dataset_filepaths(utils.DA_TACOS_BENCHMARK_CSV, "x/")) == 15000
+
+
+def test_feature_file_roundtrip(tmp_path):
+    f = {"hpcp": np.arange(24, dtype=np.float32).reshape(2, 12), "label": "W7", "track_id": "T9",
+         "madmom_features": {"onsets": np.array([1, 5, 9])}}
+    p = str(tmp_path / "W7" / "T9.h5")
+    features_io.save_features(p, f)
+    g = features_io.load_features(p)
+    np.testing.assert_array_equal(g["hpcp"], f["hpcp"])
+    assert g["label"] == "W7" and g["track_id"] == "T9"
+    np.testing.assert_array_equal(g["madmom_features"]["onsets"], [1, 5, 9])
+    with pytest.raises(IOError):
+        features_io.load_features(str(tmp_path / "missing.h5"))
+
+
+class Pairwise(CoverAlgorithm):
+    """A deterministic stand-in similarity: score(i, j) = f(i, j), not symmetric."""
+
+    def similarity(self, idxs):
+        idxs = np.asarray(idxs)
+        s = np.sin(idxs[:, 0] * 1.7 + idxs[:, 1] * 0.3).astype(np.float32)
+        for key in self.Ds:
+            self.Ds[key][idxs[:, 0], idxs[:, 1]] = s
+
+
+def _dataset(tmp_path, n_cliques=6):
+    rng = np.random.default_rng(0)
+    tracks, labels = [], []
+    for c in range(n_cliques):
+        for _ in range(2 + (c % 2)):
+            tracks.append(rng.random((50, 12)).astype(np.float32))
+            labels.append(c)
+    return synthetic.write_feature_dataset(str(tmp_path), tracks, labels)
+
+
+@pytest.mark.parametrize("symmetric", [True, False])
+def test_all_pairwise_driver(tmp_path, symmetric, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    csv, fdir = _dataset(tmp_path)
+    a = Pairwise(csv, name="Fake", datapath=fdir, shortname="t", cachedir=str(tmp_path / "cache"),
+                 similarity_types=["main", "other"])
+    a.all_pairwise(symmetric=symmetric)
+    n = a.N
+    i, j = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    f = np.sin(i * 1.7 + j * 0.3).astype(np.float32)
+    if symmetric:
+        f = np.triu(f, 1)
+        f = f + f.T
+    else:
+        np.fill_diagonal(f, 0)
+    np.testing.assert_array_equal(np.asarray(a.Ds["main"]), f)
+    # cliques were recorded in index order with the CSV's work ids
+    assert list(a.cliques) == ["W%05d" % c for c in range(6)]
+    stats = a.getEvalStatistics("main")
+    assert os.path.exists("results_t_Fake.csv")
+    # persisted matrices reload with precomputed=True
+    b = Pairwise(csv, name="Fake", datapath=fdir, shortname="t", cachedir=str(tmp_path / "cache"),
+                 similarity_types=["main", "other"])
+    b.all_pairwise(precomputed=True)
+    np.testing.assert_array_equal(np.asarray(b.Ds["main"]), f)
+    assert b.getEvalStatistics("main")[3] == stats[3]
+    a.cleanup_memmap()
+    assert not os.path.exists("%s_main_dmat" % a.get_cacheprefix())
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_worker(rank, world, port, csv, fdir, cache, out, symmetric):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    a = Pairwise(csv, name="Fake%d" % rank, datapath=fdir, shortname="w", cachedir=cache)
+    a.all_pairwise(symmetric=symmetric)
+    np.save(out % rank, np.asarray(a.Ds["main"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("symmetric", [True, False])
+def test_all_pairwise_gloo_world2_equals_world1(tmp_path, symmetric, monkeypatch):
+    import torch.multiprocessing as mp
+    monkeypatch.chdir(tmp_path)
+    csv, fdir = _dataset(tmp_path, n_cliques=9)
+    one = Pairwise(csv, name="One", datapath=fdir, shortname="w", cachedir=str(tmp_path / "c1"))
+    one.all_pairwise(symmetric=symmetric)
+    out = str(tmp_path / "rank%d.npy")
+    mp.start_processes(_rank_worker, args=(2, _free_port(), csv, fdir, str(tmp_path / "c2"), out, symmetric),
+                       nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(out % r), np.asarray(one.Ds["main"]))
+
+
+def test_resize_block_shapes():
+    from acoss.algorithms.earlyfusion_traile import resize_block
+    X = np.random.default_rng(1).random((500, 20))
+    for i1, i2, f in [(0, 100, 50), (10, 30, 50), (100, 480, 40)]:
+        r = resize_block(X, i1, i2, f)
+        assert r.shape == (f, 20) and np.all(np.isfinite(r))
+    # a constant block stays constant away from the zero-filled edges
+    r = resize_block(np.ones((400, 3)), 100, 300, 50)
+    np.testing.assert_allclose(r[10:40], 1.0, rtol=1e-12)
+
+
+def test_coverid_dispatch_errors():
+    from acoss import coverid
+    with pytest.raises(NotImplementedError):
+        coverid.benchmark("x.csv", "y/", algorithm="NoSuchAlgorithm")
+    assert coverid.algorithm_names == ["Serra09", "EarlyFusionTraile", "LateFusionChen", "FTM2D", "SiMPle"]
