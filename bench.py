@@ -149,7 +149,7 @@ def main():
     # ---- MAP / MR1 on the assembled matrix (reference normalisation + evaluation) ----
     Dfull = D.cpu().numpy()                                       # (T, T) upper triangle filled
     Dsym = (Dfull + Dfull.T).astype(np.float32)                    # all_pairwise: Ds += Ds.T (:188-191)
-    Dsym = Dsym / np.sqrt(lens.astype(np.float32))[None, :]       # Serra09.normalize_by_length (:71-83)
+    Dsym = (Dsym / np.sqrt(lens.astype(np.float64))[None, :]).astype(np.float32)  # normalize_by_length (:71-83)
     MR, MRR, MDR, MAP, tops = evaluation.eval_statistics(Dsym, labels)
 
     result = None

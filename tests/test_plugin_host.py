@@ -128,8 +128,9 @@ def test_resize_block_shapes():
     np.testing.assert_allclose(r[10:40], 1.0, rtol=1e-12)
 
 
-def test_coverid_dispatch_errors():
+def test_coverid_dispatch_errors(tmp_path, monkeypatch):
     from acoss import coverid
+    monkeypatch.chdir(tmp_path)
     with pytest.raises(NotImplementedError):
         coverid.benchmark("x.csv", "y/", algorithm="NoSuchAlgorithm")
     assert coverid.algorithm_names == ["Serra09", "EarlyFusionTraile", "LateFusionChen", "FTM2D", "SiMPle"]
