@@ -792,14 +792,17 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   if (nbmax > 65535) nbmax = 65535;
   const int64_t nb_alloc = n_pairs < nbmax ? n_pairs : nbmax;
   int64_t sub = nb_alloc;
+  // split sub-batch scratch per pair: full keys row-major (4 B), prefixes column-major (2 B) and
+  // the row-threshold words RT
+  const size_t sub_pair = 6 * (size_t)kstride + 4 * (size_t)mask_stride;
   if (split) {
-    size_t kbudget = (size_t)2 << 30;  // ~65 pairs at 2000 frames: enough blocks to fill 256 CUs
+    size_t kbudget = (size_t)2 << 30;  // ~80 pairs at 2000 frames: enough blocks to fill 256 CUs
     if (const char* e = getenv("ACOSS_KEY_BYTES")) kbudget = strtoull(e, nullptr, 10);
-    sub = (int64_t)(kbudget / (8 * (size_t)kstride));
+    sub = (int64_t)(kbudget / sub_pair);
     if (sub < 1) sub = 1;
     if (sub > nb_alloc) sub = nb_alloc;
   }
-  char* ws = static_cast<char*>(workspace(1, slot * nb_alloc + 8 * (size_t)kstride * sub + 8192));
+  char* ws = static_cast<char*>(workspace(1, slot * nb_alloc + (split ? sub_pair * sub : 0) + 8192));
   if (!ws) return ACOSS_E_HIP;
   size_t o = 0;
   auto carve = [&](size_t bytes) {
@@ -816,7 +819,8 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   uint32_t* w_mask = reinterpret_cast<uint32_t*>(carve(4 * mask_stride * nb_alloc));
   float4* w_bnd = reinterpret_cast<float4*>(carve(16 * bnd_stride * nb_alloc));
   float* w_yrot = reinterpret_cast<float*>(carve(4 * yrot_stride * nb_alloc));
-  uint16_t* w_kpl = reinterpret_cast<uint16_t*>(carve(8 * kstride * sub));
+  void* w_kpl = split ? static_cast<void*>(carve(6 * (size_t)kstride * sub)) : nullptr;
+  uint32_t* w_rt = split ? reinterpret_cast<uint32_t*>(carve(4 * (size_t)mask_stride * sub)) : nullptr;
 
   const bool eqg = params->gamma_open == params->gamma_ext;
   for (int64_t base = 0; base < n_pairs; base += nb_alloc) {
@@ -835,7 +839,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
         const int ns = (nb - s0) < sub ? (nb - s0) : (int)sub;
         CrpBatch Bs{feats, track_off, track_len, NX, ldn, pb + 2 * s0, w_oti + s0, w_dims + s0, m, tau,
                     w_yrot + (size_t)s0 * yrot_stride, yrot_stride};
-        if ((rc = launch_crp_split(Bs, ns, L, params->kappa, w_kpl, ldk, kstride,
+        if ((rc = launch_crp_split(Bs, ns, L, params->kappa, w_kpl, ldk, kstride, w_rt,
                                    w_thr_r + (size_t)s0 * thr_stride, w_T_r + (size_t)s0 * thr_stride,
                                    w_thr_c + (size_t)s0 * thr_stride, w_T_c + (size_t)s0 * thr_stride, thr_stride,
                                    w_mask + (size_t)s0 * mask_stride, mask_stride, ld, s)))

@@ -32,9 +32,9 @@ int launch_mask9(const CrpBatch& B, int nb, int L, const float* Trow, const floa
 
 // Three-kernel CRP around one sweep (crp_split.hip); 1 = not covered.
 // kplanes: 4 planes of nb*kstride uint16 (key high/low halves, row- and column-major).
-int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, uint16_t* kplanes, int ldk, int64_t kstride,
-                     float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride, uint32_t* maskT,
-                     int64_t mask_stride, int ld, hipStream_t s);
+int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, int ldk, int64_t kstride,
+                     uint32_t* RT, float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride,
+                     uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s);
 
 int launch_select16(bool trans, const CrpBatch& B, int nb, int L, float kappa, float* thr, float* T,
                     int64_t thr_stride, hipStream_t s);

@@ -6,17 +6,18 @@
 //
 //  k_sweep9      one 256-thread block per (32-row strip, pair): diagonal walk (G in
 //                registers, query frames by scalar loads, rolled reference frames in LDS);
-//                the high 16 bits of every squared-distance key go to HBM twice: row-major
-//                K16r[i][j] and column-major K16c[j][i] (through a rolling LDS tile).
-//  k_sel_rows9   one wave per CRP row: 32 keys per lane in registers, the 16-bit prefixes of
-//                the two order statistics by binary search with ballot counts (v_cmp +
-//                s_bcnt1: no cross-lane reduction), the cells sharing a prefix recomputed
-//                exactly (one per lane), rank inside the group -> percentile -> squared-domain
-//                threshold T_row.
-//  k_sel_cols9   one wave per CRP column: the same select gives T_col; lane l then holds rows
-//                32l..32l+31 of the column, i.e. exactly one 32-bit CRP word, so the mask is
-//                emitted here (key <= T_row && key <= T_col, decided on the 16-bit prefix;
-//                cells whose prefix ties a threshold prefix are recomputed exactly).
+//                every squared-distance key goes to HBM as the FULL 32-bit key row-major
+//                F[i][j] and as its HIGH 16 bits column-major Hc[j][i] (through a rolling
+//                LDS tile).
+//  k_sel_rows9   one 512-thread block per (32-row strip, pair), one wave per CRP row: 32 full
+//                keys per lane in registers, the 16-bit prefixes of the two order statistics
+//                by binary search with ballot counts (v_cmp + s_bcnt1), the tied group ranked
+//                on the exact keys -> percentile -> squared-domain threshold T_row; then the
+//                row's "key <= T_row" bits, transposed in LDS into the 32-bit strip words RT.
+//  k_sel_cols9   one wave per CRP column on the 16-bit prefixes: the same select gives T_col,
+//                the tied group's exact keys come from F (one gather round); lane l then
+//                holds rows 32l..32l+31 of the column, i.e. exactly one 32-bit CRP word:
+//                (key <= T_col bits) & RT[strip l][j].
 #include <cstdlib>
 
 #include "crp_internal.hpp"
@@ -70,12 +71,10 @@ __device__ __forceinline__ void load_query(const float* base_ptr, int f, float (
   x[8] = c.x; x[9] = c.y; x[10] = c.z; x[11] = c.w;
 }
 
-// Key planes of one pair: high / low 16 bits, row-major (line = CRP row) and column-major.
+// Key planes of one pair: full keys row-major (line = CRP row), high 16 bits column-major.
 struct KeyPlanes {
-  uint16_t* hr;
-  uint16_t* lr;
+  uint32_t* fr;
   uint16_t* hc;
-  uint16_t* lc;
 };
 
 __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride) {
@@ -91,10 +90,8 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
   float nq_r[kSR];
 #pragma unroll
   for (int r = 0; r < kSR; ++r) nq_r[r] = *(const __attribute__((address_space(4))) float*)(V.NXq + min(i0 + r, V.Mp - 1));
-  uint16_t* Hr = K.hr + (size_t)p * kstride;
-  uint16_t* Lr = K.lr + (size_t)p * kstride;
+  uint32_t* Fr = K.fr + (size_t)p * kstride;
   uint16_t* Hc = K.hc + (size_t)p * kstride;
-  uint16_t* Lc = K.lc + (size_t)p * kstride;
   for (int j0 = -(kSR - 1); j0 < V.Np; j0 += kSW) {
     __syncthreads();
     for (int e = t; e < kSYRows * 3; e += kSW) {
@@ -161,29 +158,19 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
     // consecutive rows = 64 B per column and plane) stores
     const int jj = j0 + t;
     if (jj >= 0 && jj < V.Np) {
-      for (int r = 0; r < rows; ++r) {
-        const unsigned k = tile[r][t];
-        Hr[(size_t)(i0 + r) * ldr + jj] = (uint16_t)(k >> 16);
-        Lr[(size_t)(i0 + r) * ldr + jj] = (uint16_t)(k & 0xffffu);
-      }
+      for (int r = 0; r < rows; ++r) Fr[(size_t)(i0 + r) * ldr + jj] = tile[r][t];
       unsigned col[kSR];
 #pragma unroll
       for (int r = 0; r < kSR; ++r) col[r] = tile[r][t];
       uint4* dh = reinterpret_cast<uint4*>(Hc + (size_t)jj * ldc + i0);
-      uint4* dl = reinterpret_cast<uint4*>(Lc + (size_t)jj * ldc + i0);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        uint4 h, l;
+        uint4 h;
         h.x = (col[8 * q] >> 16) | (col[8 * q + 1] & 0xffff0000u);
         h.y = (col[8 * q + 2] >> 16) | (col[8 * q + 3] & 0xffff0000u);
         h.z = (col[8 * q + 4] >> 16) | (col[8 * q + 5] & 0xffff0000u);
         h.w = (col[8 * q + 6] >> 16) | (col[8 * q + 7] & 0xffff0000u);
-        l.x = (col[8 * q] & 0xffffu) | (col[8 * q + 1] << 16);
-        l.y = (col[8 * q + 2] & 0xffffu) | (col[8 * q + 3] << 16);
-        l.z = (col[8 * q + 4] & 0xffffu) | (col[8 * q + 5] << 16);
-        l.w = (col[8 * q + 6] & 0xffffu) | (col[8 * q + 7] << 16);
         dh[q] = h;
-        dl[q] = l;
       }
     }
     __syncthreads();
@@ -247,6 +234,31 @@ struct Line {
   }
 };
 
+// A line of FULL keys (CRP row from F): v = 16-bit prefixes for the search, f = exact keys.
+template <int KPL>
+struct LineFull : Line<KPL> {
+  unsigned f[KPL];
+  __device__ __forceinline__ void load_full(const uint32_t* src, int n) {
+    const int lane = threadIdx.x & 63;
+    const int base = lane * KPL;
+    if (base + KPL <= n) {
+#pragma unroll
+      for (int q = 0; q < KPL / 4; ++q) {
+        const uint4 w = reinterpret_cast<const uint4*>(src + base)[q];
+        f[4 * q + 0] = w.x;
+        f[4 * q + 1] = w.y;
+        f[4 * q + 2] = w.z;
+        f[4 * q + 3] = w.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < KPL; ++q) f[q] = (base + q < n) ? src[base + q] : 0xffffffffu;
+    }
+#pragma unroll
+    for (int q = 0; q < KPL; ++q) this->v[q] = f[q] == 0xffffffffu ? 0xffffffffu : f[q] >> 16;
+  }
+};
+
 // Smallest prefix P with count(keys <= P) > rho.
 template <int KPL>
 __device__ __forceinline__ unsigned prefix_of_rank(const Line<KPL>& L, int rho, unsigned a, unsigned b) {
@@ -260,41 +272,92 @@ __device__ __forceinline__ unsigned prefix_of_rank(const Line<KPL>& L, int rho, 
   return a;
 }
 
-// Exact key (32 bits) of rank rho among the g keys of the line whose prefix is P; the low
-// halves come from the line's low plane `lo`. list = 64 ints of LDS owned by the wave.
-template <int KPL>
-__device__ unsigned exact_rank(const Line<KPL>& L, unsigned P, int rho, int g, const uint16_t* lo, int* list) {
+// Scratch of one wave in LDS: element list and 64 bit-words.
+struct WaveLds {
+  int list[64];
+  uint32_t words[64];
+};
+
+// Exact keys of a prefix group (the line elements whose 16-bit prefix is P), computed in ONE
+// batched round: lane k < g recomputes element list[k]. Valid when g <= 64.
+struct Group {
+  unsigned P;
+  int g;
+  int elem;      // this lane's element (lane < g)
+  unsigned key;  // its exact key (0xffffffff for lane >= g)
+};
+
+template <int KPL, class KF>
+__device__ Group group_keys(const Line<KPL>& L, unsigned P, int g, const KF& keyf, WaveLds& W) {
   const int lane = threadIdx.x & 63;
-  if (g <= 64) {
-    int base = 0;
+  int base = 0;
 #pragma unroll
-    for (int q = 0; q < KPL; ++q) {
-      const bool m = L.v[q] == P;
-      const unsigned long long bal = __ballot(m);
-      if (m)
-        list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] =
-            lane * KPL + q;
-      base += __popcll(bal);
-    }
-    __builtin_amdgcn_wave_barrier();
-    const bool act = lane < g;
-    const unsigned key = act ? ((P << 16) | (unsigned)lo[list[lane]]) : 0xffffffffu;
-    __builtin_amdgcn_wave_barrier();
-    int cl = 0, ce = 0;
-    for (int k = 0; k < g; ++k) {
-      const unsigned o = (unsigned)lane_bcast((int)key, k);
-      cl += o < key;
-      ce += o == key;
-    }
-    const int src = __builtin_ctzll(__ballot(act && cl <= rho && rho < cl + ce));
-    return (unsigned)lane_bcast((int)key, src);
+  for (int q = 0; q < KPL; ++q) {
+    const bool m = L.v[q] == P;
+    const unsigned long long bal = __ballot(m);
+    if (m)
+      W.list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] =
+          lane * KPL + q;
+    base += __popcll(bal);
   }
-  // large groups (long silences): low halves of the whole line into registers, then a
-  // binary search over the low 16 bits counting group members only
-  unsigned lw[KPL];
-  const int base = lane * KPL;
+  __builtin_amdgcn_wave_barrier();
+  Group G;
+  G.P = P;
+  G.g = g;
+  G.elem = lane < g ? W.list[lane] : 0;
+  __builtin_amdgcn_wave_barrier();
+  G.key = lane < g ? keyf(G.elem) : 0xffffffffu;
+  return G;
+}
+
+// Same group from a line that holds its exact keys in registers (no recompute).
+template <int KPL>
+__device__ Group group_keys_full(const LineFull<KPL>& L, unsigned P, int g, WaveLds& W) {
+  const int lane = threadIdx.x & 63;
+  int base = 0;
 #pragma unroll
-  for (int q = 0; q < KPL; ++q) lw[q] = (L.v[q] == P) ? (unsigned)lo[base + q] : 0x10000u;
+  for (int q = 0; q < KPL; ++q) {
+    const bool m = L.v[q] == P;
+    const unsigned long long bal = __ballot(m);
+    if (m)
+      W.list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] =
+          (int)L.f[q];
+    base += __popcll(bal);
+  }
+  __builtin_amdgcn_wave_barrier();
+  Group G;
+  G.P = P;
+  G.g = g;
+  G.elem = 0;
+  G.key = lane < g ? (unsigned)W.list[lane] : 0xffffffffu;
+  __builtin_amdgcn_wave_barrier();
+  return G;
+}
+
+// Key of rank rho (0-based) inside a batched group.
+__device__ __forceinline__ unsigned group_rank(const Group& G, int rho) {
+  const int lane = threadIdx.x & 63;
+  int cl = 0, ce = 0;
+  for (int k = 0; k < G.g; ++k) {
+    const unsigned o = (unsigned)lane_bcast((int)G.key, k);
+    cl += o < G.key;
+    ce += o == G.key;
+  }
+  const bool act = lane < G.g;
+  const int src = __builtin_ctzll(__ballot(act && cl <= rho && rho < cl + ce));
+  return (unsigned)lane_bcast((int)G.key, src);
+}
+
+// Large groups (g > 64, long silences): recompute the group's low halves lane by lane, then
+// binary-search the low 16 bits counting group members only.
+template <int KPL, class KF>
+__device__ unsigned big_group_rank(const Line<KPL>& L, unsigned P, int rho, const KF& keyf) {
+  const int base = (threadIdx.x & 63) * KPL;
+  unsigned lw[KPL];
+#pragma unroll
+  for (int q = 0; q < KPL; ++q) lw[q] = 0x10000u;
+  for (int q = 0; q < KPL; ++q)
+    if (L.v[q] == P) lw[q] = keyf(base + q) & 0xffffu;
   unsigned a = 0, b = 0xffffu;
   while (a < b) {
     const unsigned mid = (a + b) >> 1;
@@ -309,10 +372,21 @@ __device__ unsigned exact_rank(const Line<KPL>& L, unsigned P, int rho, int g, c
   return (P << 16) | a;
 }
 
-// Threshold (distance units) and squared-domain threshold of a line of n keys.
-template <int KPL>
-__device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const uint16_t* lo_plane, int* list,
-                               float* thr, float* T) {
+template <int KPL, class KF>
+__device__ unsigned rank_in_prefix(const Line<KPL>& L, unsigned P, int rho, int g, const KF& keyf, WaveLds& W,
+                                   Group* cache) {
+  if (g <= 64) {
+    if (cache->g < 0 || cache->P != P) *cache = group_keys(L, P, g, keyf, W);
+    return group_rank(*cache, rho);
+  }
+  return big_group_rank(L, P, rho, keyf);
+}
+
+// Threshold (distance units) and squared-domain threshold of a line of n keys; leaves the
+// exact keys of the last batched group in *cache for le_bits.
+template <int KPL, class KF>
+__device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF& keyf, WaveLds& W, Group* c_lo,
+                               Group* c_hi, float* thr, float* T) {
   const float q = (float)(n - 1) * kappa;
   const float lo_f = floorf(q), hi_f = ceilf(q);
   const int lo = (int)lo_f, hi = (int)hi_f;
@@ -321,14 +395,14 @@ __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const uin
   const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax);
   const int le = L.count_le(Pl);
   const int less = Pl > kmin ? L.count_le(Pl - 1) : 0;
-  const unsigned vlo = exact_rank(L, Pl, lo - less, le - less, lo_plane, list);
+  const unsigned vlo = rank_in_prefix(L, Pl, lo - less, le - less, keyf, W, c_lo);
   unsigned vhi = vlo;
   if (hi != lo) {
     if (hi < le) {
-      vhi = exact_rank(L, Pl, hi - less, le - less, lo_plane, list);
+      vhi = rank_in_prefix(L, Pl, hi - less, le - less, keyf, W, c_lo);
     } else {
       const unsigned Ph = L.min_greater(Pl);
-      vhi = exact_rank(L, Ph, 0, L.count_le(Ph) - le, lo_plane, list);
+      vhi = rank_in_prefix(L, Ph, 0, L.count_le(Ph) - le, keyf, W, c_hi);
     }
   }
   const float slo = sqrt_rn(__builtin_bit_cast(float, vlo));
@@ -345,107 +419,206 @@ __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const uin
   *T = sq_threshold(th);
 }
 
-// ---------------------------------------------------------------------------------------
-// k_sel_rows9<KPL>: one wave per CRP row.
-// ---------------------------------------------------------------------------------------
+// Row variant of line_threshold: the line holds its exact keys, groups rank from registers;
+// groups above 64 members binary-search the low halves held in registers.
 template <int KPL>
-__global__ __launch_bounds__(256) void k_sel_rows9(CrpBatch B, KeyPlanes K, int ldr, int64_t kstride, float kappa,
+__device__ unsigned row_rank(const LineFull<KPL>& L, unsigned P, int rho, int g, WaveLds& W) {
+  if (g <= 64) return group_rank(group_keys_full(L, P, g, W), rho);
+  unsigned a = 0, b = 0xffffu;
+  while (a < b) {
+    const unsigned mid = (a + b) >> 1;
+    int c = 0;
+#pragma unroll
+    for (int q = 0; q < KPL; ++q) c += __popcll(__ballot(L.v[q] == P && (L.f[q] & 0xffffu) <= mid));
+    if (c > rho)
+      b = mid;
+    else
+      a = mid + 1;
+  }
+  return (P << 16) | a;
+}
+
+template <int KPL>
+__device__ void row_threshold(const LineFull<KPL>& L, int n, float kappa, WaveLds& W, float* thr, float* T) {
+  const float q = (float)(n - 1) * kappa;
+  const float lo_f = floorf(q), hi_f = ceilf(q);
+  const int lo = (int)lo_f, hi = (int)hi_f;
+  unsigned kmin, kmax;
+  L.min_max(&kmin, &kmax);
+  const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax);
+  const int le = L.count_le(Pl);
+  const int less = Pl > kmin ? L.count_le(Pl - 1) : 0;
+  const unsigned vlo = row_rank(L, Pl, lo - less, le - less, W);
+  unsigned vhi = vlo;
+  if (hi != lo) {
+    if (hi < le) {
+      vhi = row_rank(L, Pl, hi - less, le - less, W);
+    } else {
+      const unsigned Ph = L.min_greater(Pl);
+      vhi = row_rank(L, Ph, 0, L.count_le(Ph) - le, W);
+    }
+  }
+  const float slo = sqrt_rn(__builtin_bit_cast(float, vlo));
+  float th;
+  if (lo_f == hi_f) {
+    th = slo;
+  } else {
+    const float shi = sqrt_rn(__builtin_bit_cast(float, vhi));
+    const float aa = slo * (hi_f - q);
+    const float bb = shi * (q - lo_f);
+    th = aa + bb;
+  }
+  *thr = th;
+  *T = sq_threshold(th);
+}
+
+// Bits of "key <= T" for the KPL elements of this lane (element e = lane*KPL + q). Decided on
+// the prefix; the elements whose prefix equals T's are decided on exact keys from a batched
+// group (reused from the threshold search when it has that prefix).
+template <int KPL, class KF>
+__device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, WaveLds& W, const Group& c_lo,
+                            const Group& c_hi) {
+  const unsigned T16 = Tbits >> 16;
+  const int lane = threadIdx.x & 63;
+  uint32_t word = 0;
+  int amb = 0;
+#pragma unroll
+  for (int q = 0; q < KPL; ++q) {
+    const unsigned k = L.v[q];  // 0xffffffff (no element) is never <= T16
+    word |= (uint32_t)(k < T16) << q;
+    amb += k == T16;
+  }
+  const int g = wave_sum(amb);
+  if (g == 0) return word;
+  if (g <= 64) {
+    Group G;
+    if (c_lo.g >= 0 && c_lo.P == T16)
+      G = c_lo;
+    else if (c_hi.g >= 0 && c_hi.P == T16)
+      G = c_hi;
+    else
+      G = group_keys(L, T16, g, keyf, W);
+    W.words[lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (lane < G.g && G.key <= Tbits) atomicOr(&W.words[G.elem / KPL], 1u << (G.elem % KPL));
+    __builtin_amdgcn_wave_barrier();
+    return word | W.words[lane];
+  }
+  const int base = lane * KPL;
+  for (int q = 0; q < KPL; ++q)
+    if (L.v[q] == T16) word |= (uint32_t)(keyf(base + q) <= Tbits) << q;
+  return word;
+}
+
+// ---------------------------------------------------------------------------------------
+// k_sel_rows9: one 512-thread block per (32-row strip, pair); wave w takes rows w, w+8, ...
+// Emits T_row and the strip's row-threshold words RT[strip][j] (bit r: key(i0+r, j) <= T_row).
+// ---------------------------------------------------------------------------------------
+constexpr int kRowWaves = 8;
+
+__global__ __launch_bounds__(512, 4) void k_sel_rows9(CrpBatch B, KeyPlanes K, int ldr, int64_t kstride, float kappa,
                                                    float* __restrict__ thr, float* __restrict__ Tq,
-                                                   int64_t thr_stride) {
-  __shared__ int lists[4][64];
+                                                   int64_t thr_stride, uint32_t* __restrict__ RT,
+                                                   int64_t rt_stride, int ld) {
+  constexpr int KPL = 32;
+  __shared__ WaveLds wl[kRowWaves];
+  __shared__ uint32_t rowbits[kSR][64];
   const int p = blockIdx.y;
   const PairView V = pair_view(B, p);
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= V.Mp) return;
-  int* list = lists[threadIdx.x >> 6];
-  const int lane = threadIdx.x & 63;
-  Line<KPL> L;
-  const size_t line = (size_t)p * kstride + (size_t)i * ldr;
-  L.load(K.hr + line, V.Np);
-  float th, T;
-  line_threshold(L, V.Np, kappa, K.lr + line, list, &th, &T);
-  if (lane == 0) {
-    thr[(size_t)p * thr_stride + i] = th;
-    Tq[(size_t)p * thr_stride + i] = T;
+  const int strip = blockIdx.x, i0 = strip * kSR;
+  if (i0 >= V.Mp) return;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  WaveLds& W = wl[w];
+#pragma unroll 1
+  for (int r = w; r < kSR; r += kRowWaves) {
+    const int i = i0 + r;
+    uint32_t word = 0;
+    if (i < V.Mp) {
+      LineFull<KPL> L;
+      L.load_full(K.fr + (size_t)p * kstride + (size_t)i * ldr, V.Np);
+      float th, T;
+      row_threshold(L, V.Np, kappa, W, &th, &T);
+      if (lane == 0) {
+        thr[(size_t)p * thr_stride + i] = th;
+        Tq[(size_t)p * thr_stride + i] = T;
+      }
+      const unsigned Tb = __builtin_bit_cast(unsigned, T);
+#pragma unroll
+      for (int q = 0; q < KPL; ++q) word |= (uint32_t)(L.f[q] <= Tb) << q;  // 0xffffffff never <= T
+    }
+    rowbits[r][lane] = word;
+  }
+  __syncthreads();
+  // transpose: word of column j = bit (j & 31) of rowbits[r][j >> 5], r = 0..31
+  uint32_t* out = RT + (size_t)p * rt_stride + (size_t)strip * ld;
+  for (int j = threadIdx.x; j < V.Np; j += 512) {
+    const int l = j >> 5, q = j & 31;
+    uint32_t word = 0;
+#pragma unroll
+    for (int r = 0; r < kSR; ++r) word |= ((rowbits[r][l] >> q) & 1u) << r;
+    out[j] = word;
   }
 }
 
 // ---------------------------------------------------------------------------------------
-// k_sel_cols9<KPL>: one wave per CRP column; also emits the CRP words of the column.
-// Requires KPL == 32 for the word emission (lane l <-> rows 32l..32l+31).
+// k_sel_cols9: one wave per CRP column; emits T_col and the column's CRP words.
+// Lane l <-> rows 32l..32l+31 (KPL == 32).
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
-                                                   const float* __restrict__ Trow,
-                                                   float* __restrict__ thr, float* __restrict__ Tq,
-                                                   int64_t thr_stride, uint32_t* __restrict__ maskT,
-                                                   int64_t mask_stride, int ld) {
+                                                   const uint32_t* __restrict__ RT, float* __restrict__ thr,
+                                                   float* __restrict__ Tq, int64_t thr_stride,
+                                                   uint32_t* __restrict__ maskT, int64_t mask_stride, int ld) {
   constexpr int KPL = 32;
-  __shared__ int lists[4][64];
+  __shared__ WaveLds wl[4];
   const int p = blockIdx.y;
   const PairView V = pair_view(B, p);
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= V.Np) return;
-  int* list = lists[threadIdx.x >> 6];
+  WaveLds& W = wl[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
   Line<KPL> L;
   const size_t line = (size_t)p * kstride + (size_t)j * ldc;
   L.load(K.hc + line, V.Mp);
-  const uint16_t* lo_plane = K.lc + line;
+  const uint32_t* Fcol = K.fr + (size_t)p * kstride + j;
+  auto keyf = [&](int e) { return Fcol[(size_t)e * ldc]; };
   float th, Tc;
-  line_threshold(L, V.Mp, kappa, lo_plane, list, &th, &Tc);
+  Group c_lo, c_hi;
+  c_lo.g = c_hi.g = -1;
+  line_threshold(L, V.Mp, kappa, keyf, W, &c_lo, &c_hi, &th, &Tc);
   if (lane == 0) {
     thr[(size_t)p * thr_stride + j] = th;
     Tq[(size_t)p * thr_stride + j] = Tc;
   }
-  // CRP word of strip `lane` (rows 32*lane .. +31) at column j
-  const int i0 = lane * KPL;
-  if (i0 >= V.Mp) return;
-  const unsigned Tc_bits = __builtin_bit_cast(unsigned, Tc);
-  const unsigned Tc16 = Tc_bits >> 16;
-  const float* tr = Trow + (size_t)p * thr_stride + i0;
-  uint32_t word = 0, amb = 0;
-#pragma unroll
-  for (int q = 0; q < KPL; ++q) {
-    const unsigned k = L.v[q];
-    if (k == 0xffffffffu) continue;
-    const unsigned Tr_bits = __builtin_bit_cast(unsigned, tr[q]);
-    const unsigned Tr16 = Tr_bits >> 16;
-    const bool surely = (k < Tr16) && (k < Tc16);
-    const bool maybe = (k <= Tr16) && (k <= Tc16);
-    word |= (uint32_t)surely << q;
-    amb |= (uint32_t)(maybe && !surely) << q;
-  }
-  while (amb) {  // prefix ties a threshold prefix: decide on the exact key
-    const int q = __builtin_ctz(amb);
-    amb &= amb - 1;
-    const unsigned key = (L.v[q] << 16) | (unsigned)lo_plane[i0 + q];
-    const unsigned Tr_bits = __builtin_bit_cast(unsigned, tr[q]);
-    word |= (uint32_t)((key <= Tr_bits) && (key <= Tc_bits)) << q;
-  }
-  maskT[(size_t)p * mask_stride + (size_t)lane * ld + j] = word;
+  const size_t w = (size_t)p * mask_stride + (size_t)lane * ld + j;
+  const uint32_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
+  if (lane * KPL >= V.Mp) return;
+  maskT[w] = bits & RT[w];
 }
 
 }  // namespace
 
 // Three-kernel CRP (m = 9, lines up to 2048 keys). Returns 1 if not applicable.
-int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, uint16_t* kplanes, int ldk, int64_t kstride,
-                     float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride, uint32_t* maskT,
-                     int64_t mask_stride, int ld, hipStream_t s) {
+// kplanes: nb * kstride uint32 full keys, then nb * kstride uint16 prefixes; RT: nb * mask_stride
+// words (same layout as maskT).
+int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, int ldk, int64_t kstride,
+                     uint32_t* RT, float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride,
+                     uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s) {
   if (B.m != kMS || L > 2048) return 1;
   const size_t plane = (size_t)nb * kstride;
-  const KeyPlanes K{kplanes, kplanes + plane, kplanes + 2 * plane, kplanes + 3 * plane};
+  const KeyPlanes K{static_cast<uint32_t*>(kplanes), reinterpret_cast<uint16_t*>(static_cast<uint32_t*>(kplanes) + plane)};
+  const int nstrips = (L + kSR - 1) / kSR;
   prof_begin(PH_SWEEP, s);
-  hipLaunchKernelGGL(k_sweep9, dim3((L + kSR - 1) / kSR, nb), dim3(kSW), 0, s, B, K, ldk, ldk, kstride);
+  hipLaunchKernelGGL(k_sweep9, dim3(nstrips, nb), dim3(kSW), 0, s, B, K, ldk, ldk, kstride);
   ACOSS_LAUNCH_CHECK();
   prof_end(PH_SWEEP, s);
   prof_begin(PH_SEL_ROWS, s);
-  hipLaunchKernelGGL(k_sel_rows9<32>, dim3((L + 3) / 4, nb), dim3(256), 0, s, B, K, ldk, kstride, kappa, thr_r, T_r,
-                     thr_stride);
+  hipLaunchKernelGGL(k_sel_rows9, dim3(nstrips, nb), dim3(512), 0, s, B, K, ldk, kstride, kappa, thr_r, T_r,
+                     thr_stride, RT, mask_stride, ld);
   ACOSS_LAUNCH_CHECK();
   prof_end(PH_SEL_ROWS, s);
   prof_begin(PH_SEL_COLS, s);
-  hipLaunchKernelGGL(k_sel_cols9, dim3((L + 3) / 4, nb), dim3(256), 0, s, B, K, ldk, kstride, kappa, T_r, thr_c,
-                     T_c, thr_stride, maskT, mask_stride, ld);
+  hipLaunchKernelGGL(k_sel_cols9, dim3((L + 3) / 4, nb), dim3(256), 0, s, B, K, ldk, kstride, kappa, RT, thr_c, T_c,
+                     thr_stride, maskT, mask_stride, ld);
   ACOSS_LAUNCH_CHECK();
   prof_end(PH_SEL_COLS, s);
   return ACOSS_OK;
