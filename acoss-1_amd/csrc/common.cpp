@@ -60,6 +60,34 @@ void* workspace(int slot, size_t bytes) {
   return b.ptr;
 }
 
+// One extra stream and a few timing-free events per device, for overlapping independent
+// sub-batches inside one ABI call (the caller's stream stays the ordering point).
+hipStream_t side_stream() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  static std::map<int, hipStream_t> streams;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = streams.find(dev);
+  if (it != streams.end()) return it->second;
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  streams[dev] = st;
+  return st;
+}
+
+hipEvent_t sync_event(int idx) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  static std::map<std::pair<int, int>, hipEvent_t> evs;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = evs.find({dev, idx});
+  if (it != evs.end()) return it->second;
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  evs[{dev, idx}] = e;
+  return e;
+}
+
 int release_all_workspaces() {
   std::lock_guard<std::mutex> lk(g_mu);
   if (hipDeviceSynchronize() != hipSuccess) return ACOSS_E_HIP;

@@ -16,6 +16,8 @@ void clear_error();
 // contents are not preserved on growth). Returns nullptr (and sets the error) on failure.
 void* workspace(int slot, size_t bytes);
 int release_all_workspaces();
+hipStream_t side_stream();      // per-device helper stream (non-blocking)
+hipEvent_t sync_event(int idx);  // per-device timing-free events for cross-stream ordering
 
 // Optional per-phase timing with HIP events recorded on the launch stream (bench.py reads it
 // through acoss_profile_read). Phases are small integers; names in common.cpp.

@@ -802,7 +802,14 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
     if (sub < 1) sub = 1;
     if (sub > nb_alloc) sub = nb_alloc;
   }
-  char* ws = static_cast<char*>(workspace(1, slot * nb_alloc + (split ? sub_pair * sub : 0) + 8192));
+  // split sub-batches alternate between the caller's stream and a side stream, each with its
+  // own key-plane buffer, so one sub-batch's selects overlap the next one's sweep
+  static const int nbuf = [] {
+    const char* e = getenv("ACOSS_SPLIT_STREAMS");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : (v > 2 ? 2 : v);
+  }();
+  char* ws = static_cast<char*>(workspace(1, slot * nb_alloc + (split ? nbuf * sub_pair * sub : 0) + 8192));
   if (!ws) return ACOSS_E_HIP;
   size_t o = 0;
   auto carve = [&](size_t bytes) {
@@ -819,8 +826,20 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   uint32_t* w_mask = reinterpret_cast<uint32_t*>(carve(4 * mask_stride * nb_alloc));
   float4* w_bnd = reinterpret_cast<float4*>(carve(16 * bnd_stride * nb_alloc));
   float* w_yrot = reinterpret_cast<float*>(carve(4 * yrot_stride * nb_alloc));
-  void* w_kpl = split ? static_cast<void*>(carve(6 * (size_t)kstride * sub)) : nullptr;
-  uint32_t* w_rt = split ? reinterpret_cast<uint32_t*>(carve(4 * (size_t)mask_stride * sub)) : nullptr;
+  void* w_kpl[2] = {nullptr, nullptr};
+  uint32_t* w_rt[2] = {nullptr, nullptr};
+  for (int b = 0; split && b < nbuf; ++b) {
+    w_kpl[b] = static_cast<void*>(carve(6 * (size_t)kstride * sub));
+    w_rt[b] = reinterpret_cast<uint32_t*>(carve(4 * (size_t)mask_stride * sub));
+  }
+  hipStream_t ss[2] = {s, s};
+  if (split && nbuf == 2) {
+    ss[1] = side_stream();
+    if (!ss[1]) {
+      set_error("could not create the side stream");
+      return ACOSS_E_HIP;
+    }
+  }
 
   const bool eqg = params->gamma_open == params->gamma_ext;
   for (int64_t base = 0; base < n_pairs; base += nb_alloc) {
@@ -835,15 +854,28 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_OTI, s);
     if (split) {
-      for (int s0 = 0; s0 < nb; s0 += (int)sub) {
+      const bool two = nbuf == 2 && nb > sub;
+      if (two) {  // the side stream starts after this batch's OTI / roll on the caller's stream
+        hipEvent_t e0 = sync_event(0);
+        ACOSS_HIP_CHECK(hipEventRecord(e0, s));
+        ACOSS_HIP_CHECK(hipStreamWaitEvent(ss[1], e0, 0));
+      }
+      int k = 0;
+      for (int s0 = 0; s0 < nb; s0 += (int)sub, ++k) {
         const int ns = (nb - s0) < sub ? (nb - s0) : (int)sub;
+        const int b = two ? (k & 1) : 0;
         CrpBatch Bs{feats, track_off, track_len, NX, ldn, pb + 2 * s0, w_oti + s0, w_dims + s0, m, tau,
                     w_yrot + (size_t)s0 * yrot_stride, yrot_stride};
-        if ((rc = launch_crp_split(Bs, ns, L, params->kappa, w_kpl, ldk, kstride, w_rt,
+        if ((rc = launch_crp_split(Bs, ns, L, params->kappa, w_kpl[b], ldk, kstride, w_rt[b],
                                    w_thr_r + (size_t)s0 * thr_stride, w_T_r + (size_t)s0 * thr_stride,
                                    w_thr_c + (size_t)s0 * thr_stride, w_T_c + (size_t)s0 * thr_stride, thr_stride,
-                                   w_mask + (size_t)s0 * mask_stride, mask_stride, ld, s)))
+                                   w_mask + (size_t)s0 * mask_stride, mask_stride, ld, ss[b])))
           return rc;
+      }
+      if (two) {  // the DP (caller's stream) needs every sub-batch of both streams
+        hipEvent_t e1 = sync_event(1);
+        ACOSS_HIP_CHECK(hipEventRecord(e1, ss[1]));
+        ACOSS_HIP_CHECK(hipStreamWaitEvent(s, e1, 0));
       }
     } else {
       CrpBatch B{feats, track_off, track_len, NX, ldn, pb, w_oti, w_dims, m, tau, w_yrot, yrot_stride};

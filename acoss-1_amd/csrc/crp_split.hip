@@ -59,7 +59,7 @@ __device__ __forceinline__ PairView pair_view(const CrpBatch& B, int p) {
 constexpr int kSR = 32;                       // rows per strip
 constexpr int kSW = 256;                      // diagonals per panel
 constexpr int kSYRows = kSW + kSR + kMS - 2;  // 295 reference frames per panel
-constexpr int kSCols = kSW + kSR;             // 288 columns touched (+1 pad)
+constexpr int kSCols = kSW + kSR;             // 288 columns touched
 
 __device__ __forceinline__ void load_query(const float* base_ptr, int f, float (&x)[12]) {
   const float* base = base_ptr + (size_t)f * 12;
@@ -77,10 +77,12 @@ struct KeyPlanes {
   uint16_t* hc;
 };
 
+constexpr int kTP = 34;  // tile pitch in halfwords: 17 words, odd -> lane stride hits distinct banks
+
 __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride) {
   __shared__ __attribute__((aligned(16))) float Ys[kSYRows * 12];
   __shared__ float Ns[kSCols];
-  __shared__ __attribute__((aligned(16))) uint32_t tile[kSR][kSCols + 4];  // rolling full-key tile
+  __shared__ __attribute__((aligned(16))) uint16_t tileT[kSCols * kTP];  // [column][row] 16-bit prefixes
   const int p = blockIdx.y;
   const PairView V = pair_view(B, p);
   const int strip = blockIdx.x, i0 = strip * kSR;
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
   float nq_r[kSR];
 #pragma unroll
   for (int r = 0; r < kSR; ++r) nq_r[r] = *(const __attribute__((address_space(4))) float*)(V.NXq + min(i0 + r, V.Mp - 1));
-  uint32_t* Fr = K.fr + (size_t)p * kstride;
+  uint32_t* Fr = K.fr + (size_t)p * kstride + (size_t)i0 * ldr;
   uint16_t* Hc = K.hc + (size_t)p * kstride;
   for (int j0 = -(kSR - 1); j0 < V.Np; j0 += kSW) {
     __syncthreads();
@@ -149,34 +151,35 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
 #pragma unroll
         for (int u = 0; u < kMS; ++u) dot = dot + gw[(r + u) % kMS];
         const float d2 = (nq_r[r] - 2.0f * dot) + Ns[t + r];
-        const float key = d2 > 0.0f ? d2 : 0.0f;
-        tile[r][t + r] = __builtin_bit_cast(unsigned, key);
+        const unsigned key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
+        // full key row-major straight from registers: the 64 lanes write 64 consecutive columns
+        const int col = j0 + t + r;
+        if (r < rows && col >= 0 && col < V.Np) Fr[(size_t)r * ldr + col] = key;
+        tileT[(t + r) * kTP + r] = (uint16_t)(key >> 16);
       }
     }
     __syncthreads();
-    // columns [j0, j0 + 256) complete: row-major (coalesced along j) and column-major (32
-    // consecutive rows = 64 B per column and plane) stores
+    // columns [j0, j0 + 256) complete: column-major prefixes, 32 rows = 64 B per column
     const int jj = j0 + t;
     if (jj >= 0 && jj < V.Np) {
-      for (int r = 0; r < rows; ++r) Fr[(size_t)(i0 + r) * ldr + jj] = tile[r][t];
-      unsigned col[kSR];
-#pragma unroll
-      for (int r = 0; r < kSR; ++r) col[r] = tile[r][t];
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(tileT + t * kTP);
       uint4* dh = reinterpret_cast<uint4*>(Hc + (size_t)jj * ldc + i0);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         uint4 h;
-        h.x = (col[8 * q] >> 16) | (col[8 * q + 1] & 0xffff0000u);
-        h.y = (col[8 * q + 2] >> 16) | (col[8 * q + 3] & 0xffff0000u);
-        h.z = (col[8 * q + 4] >> 16) | (col[8 * q + 5] & 0xffff0000u);
-        h.w = (col[8 * q + 6] >> 16) | (col[8 * q + 7] & 0xffff0000u);
+        h.x = src[4 * q];
+        h.y = src[4 * q + 1];
+        h.z = src[4 * q + 2];
+        h.w = src[4 * q + 3];
         dh[q] = h;
       }
     }
     __syncthreads();
     // roll the 31-column tail to the front
-    if (t < kSR - 1)
-      for (int r = 0; r < kSR; ++r) tile[r][t] = tile[r][kSW + t];
+    for (int e = t; e < (kSR - 1) * (kTP / 2); e += kSW) {
+      const int c = e / (kTP / 2), w = e - c * (kTP / 2);
+      reinterpret_cast<uint32_t*>(tileT)[c * (kTP / 2) + w] = reinterpret_cast<const uint32_t*>(tileT)[(kSW + c) * (kTP / 2) + w];
+    }
   }
 }
 

@@ -1,0 +1,4 @@
+set -e
+cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python -m pytest tests/test_gpu_crp.py -x -q -m gpu 2>&1 | tail -2
+for NS in 1 2; do echo "streams=$NS"; ACOSS_SPLIT_STREAMS=$NS timeout -k 10 120 python tools/kbench.py --pairs 13366 --reps 3 2>&1 | grep -E "rep 2|checksum"; done
