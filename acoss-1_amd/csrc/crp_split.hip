@@ -190,6 +190,7 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
 template <int KPL>
 struct Line {
   unsigned v[KPL];
+  unsigned pv[KPL / 2];  // prefixes packed in pairs, 15-bit fields + guard bit (0x7fff = none)
   __device__ __forceinline__ void load(const uint16_t* src, int n) {
     const int lane = threadIdx.x & 63;
     const int base = lane * KPL;
@@ -210,13 +211,25 @@ struct Line {
 #pragma unroll
       for (int q = 0; q < KPL; ++q) v[q] = (base + q < n) ? (unsigned)src[base + q] : 0xffffffffu;
     }
+    pack();
   }
-  // #keys <= x (x <= 0xffff): ballot per slot, popcount on the scalar unit
-  __device__ __forceinline__ int count_le(unsigned x) const {
-    int c = 0;
+  __device__ __forceinline__ void pack() {
 #pragma unroll
-    for (int q = 0; q < KPL; ++q) c += __popcll(__ballot(v[q] <= x));
-    return c;
+    for (int h = 0; h < KPL / 2; ++h) {
+      const unsigned a = v[2 * h] > 0x7fffu ? 0x7fffu : v[2 * h];
+      const unsigned b = v[2 * h + 1] > 0x7fffu ? 0x7fffu : v[2 * h + 1];
+      pv[h] = a | (b << 16);
+    }
+  }
+  // #keys <= x (x <= 0x7fff; real key prefixes are <= 0x7f80, the sign bit is 0): per field
+  // (x + 0x8000) - a keeps bit 15 iff a <= x, with no borrow across fields; popcount on VALU,
+  // one DPP wave sum (no SGPR per compare, no SALU).
+  __device__ __forceinline__ int count_le(unsigned x) const {
+    const unsigned X2 = (x + 0x8000u) * 0x10001u;
+    unsigned c = 0;
+#pragma unroll
+    for (int h = 0; h < KPL / 2; ++h) c = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c;
+    return wave_sum((int)c);
   }
   __device__ __forceinline__ void min_max(unsigned* mn, unsigned* mx) const {
     unsigned a = 0xffffu, b = 0u;
@@ -259,6 +272,7 @@ struct LineFull : Line<KPL> {
     }
 #pragma unroll
     for (int q = 0; q < KPL; ++q) this->v[q] = f[q] == 0xffffffffu ? 0xffffffffu : f[q] >> 16;
+    this->pack();
   }
 };
 
