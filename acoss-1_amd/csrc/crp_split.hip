@@ -7,8 +7,8 @@
 //  k_sweep9      one 256-thread block per (32-row strip, pair): diagonal walk (G in
 //                registers, query frames by scalar loads, rolled reference frames in LDS);
 //                every squared-distance key goes to HBM as the FULL 32-bit key row-major
-//                F[i][j] and as its HIGH 16 bits column-major Hc[j][i] (through a rolling
-//                LDS tile).
+//                F[i][j] and as its HIGH 16 bits strip-major Hc[i/32][j][i%32] (64 B per
+//                column and strip, a block's columns contiguous; through a rolling LDS tile).
 //  k_sel_rows9   one 512-thread block per (32-row strip, pair), one wave per CRP row: 32 full
 //                keys per lane in registers, the 16-bit prefixes of the two order statistics
 //                by binary search with ballot counts (v_cmp + s_bcnt1), the tied group ranked
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
     const int jj = j0 + t;
     if (jj >= 0 && jj < V.Np) {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(tileT + t * kTP);
-      uint4* dh = reinterpret_cast<uint4*>(Hc + (size_t)jj * ldc + i0);
+      uint4* dh = reinterpret_cast<uint4*>(Hc + ((size_t)strip * ldc + jj) * kSR);  // [strip][column][32 rows]
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         uint4 h;
@@ -210,6 +210,30 @@ struct Line {
     } else {
 #pragma unroll
       for (int q = 0; q < KPL; ++q) v[q] = (base + q < n) ? (unsigned)src[base + q] : 0xffffffffu;
+    }
+    pack();
+  }
+  // lane l's KPL elements start at src_l = col0 + l * lane_stride (strip-major column plane)
+  __device__ __forceinline__ void load_lanes(const uint16_t* col0, size_t lane_stride, int n) {
+    const int lane = threadIdx.x & 63;
+    const int base = lane * KPL;
+    const uint16_t* src = col0 + (size_t)lane * lane_stride;
+    if (base + KPL <= n) {
+#pragma unroll
+      for (int q = 0; q < KPL / 8; ++q) {
+        const uint4 w = reinterpret_cast<const uint4*>(src)[q];
+        v[8 * q + 0] = w.x & 0xffffu;
+        v[8 * q + 1] = w.x >> 16;
+        v[8 * q + 2] = w.y & 0xffffu;
+        v[8 * q + 3] = w.y >> 16;
+        v[8 * q + 4] = w.z & 0xffffu;
+        v[8 * q + 5] = w.z >> 16;
+        v[8 * q + 6] = w.w & 0xffffu;
+        v[8 * q + 7] = w.w >> 16;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < KPL; ++q) v[q] = (base + q < n) ? (unsigned)src[q] : 0xffffffffu;
     }
     pack();
   }
@@ -594,8 +618,7 @@ __global__ __launch_bounds__(256) void k_sel_cols9(CrpBatch B, KeyPlanes K, int 
   WaveLds& W = wl[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
   Line<KPL> L;
-  const size_t line = (size_t)p * kstride + (size_t)j * ldc;
-  L.load(K.hc + line, V.Mp);
+  L.load_lanes(K.hc + (size_t)p * kstride + (size_t)j * kSR, (size_t)ldc * kSR, V.Mp);
   const uint32_t* Fcol = K.fr + (size_t)p * kstride + j;
   auto keyf = [&](int e) { return Fcol[(size_t)e * ldc]; };
   float th, Tc;
