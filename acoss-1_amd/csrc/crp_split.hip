@@ -185,35 +185,31 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
 
 // ---------------------------------------------------------------------------------------
 // Per-wave select on one line (CRP row or column) of 16-bit key prefixes.
-// Lane l holds keys [l*KPL, (l+1)*KPL) (0xffffffff = no element).
+// Lane l holds elements [l*KPL, (l+1)*KPL) as KPL/2 packed words: element 2h in bits 0..15,
+// 2h+1 in bits 16..31. Real prefixes are <= 0x7f80 (keys are >= +0, the sign bit is 0), so
+// 0x7fff marks "no element" and every field keeps a free guard bit for SWAR arithmetic.
 // ---------------------------------------------------------------------------------------
+constexpr unsigned kNone = 0x7fffu;
+
+__device__ __forceinline__ unsigned pk_min_u16(unsigned a, unsigned b) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ unsigned pk_max_u16(unsigned a, unsigned b) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ unsigned pk_add_u16(unsigned a, unsigned b) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+
 template <int KPL>
 struct Line {
-  unsigned v[KPL];
-  unsigned pv[KPL / 2];  // prefixes packed in pairs, 15-bit fields + guard bit (0x7fff = none)
-  __device__ __forceinline__ void load(const uint16_t* src, int n) {
-    const int lane = threadIdx.x & 63;
-    const int base = lane * KPL;
-    if (base + KPL <= n) {
-#pragma unroll
-      for (int q = 0; q < KPL / 8; ++q) {
-        const uint4 w = reinterpret_cast<const uint4*>(src + base)[q];
-        v[8 * q + 0] = w.x & 0xffffu;
-        v[8 * q + 1] = w.x >> 16;
-        v[8 * q + 2] = w.y & 0xffffu;
-        v[8 * q + 3] = w.y >> 16;
-        v[8 * q + 4] = w.z & 0xffffu;
-        v[8 * q + 5] = w.z >> 16;
-        v[8 * q + 6] = w.w & 0xffffu;
-        v[8 * q + 7] = w.w >> 16;
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < KPL; ++q) v[q] = (base + q < n) ? (unsigned)src[base + q] : 0xffffffffu;
-    }
-    pack();
-  }
-  // lane l's KPL elements start at src_l = col0 + l * lane_stride (strip-major column plane)
+  unsigned pv[KPL / 2];
+  __device__ __forceinline__ unsigned pfx(int q) const { return (q & 1) ? (pv[q >> 1] >> 16) : (pv[q >> 1] & 0xffffu); }
+  // lane l's KPL elements start at col0 + l * lane_stride (strip-major column plane): the
+  // loaded words already are the packed pairs
   __device__ __forceinline__ void load_lanes(const uint16_t* col0, size_t lane_stride, int n) {
     const int lane = threadIdx.x & 63;
     const int base = lane * KPL;
@@ -222,32 +218,27 @@ struct Line {
 #pragma unroll
       for (int q = 0; q < KPL / 8; ++q) {
         const uint4 w = reinterpret_cast<const uint4*>(src)[q];
-        v[8 * q + 0] = w.x & 0xffffu;
-        v[8 * q + 1] = w.x >> 16;
-        v[8 * q + 2] = w.y & 0xffffu;
-        v[8 * q + 3] = w.y >> 16;
-        v[8 * q + 4] = w.z & 0xffffu;
-        v[8 * q + 5] = w.z >> 16;
-        v[8 * q + 6] = w.w & 0xffffu;
-        v[8 * q + 7] = w.w >> 16;
+        pv[4 * q + 0] = w.x;
+        pv[4 * q + 1] = w.y;
+        pv[4 * q + 2] = w.z;
+        pv[4 * q + 3] = w.w;
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < KPL; ++q) v[q] = (base + q < n) ? (unsigned)src[q] : 0xffffffffu;
+      for (int h = 0; h < KPL / 2; ++h) {
+        const unsigned a = (base + 2 * h < n) ? (unsigned)src[2 * h] : kNone;
+        const unsigned b = (base + 2 * h + 1 < n) ? (unsigned)src[2 * h + 1] : kNone;
+        pv[h] = a | (b << 16);
+      }
     }
-    pack();
   }
-  __device__ __forceinline__ void pack() {
+  // from full keys (0xffffffff = none): high halves of two keys in one v_perm, clamped to kNone
+  __device__ __forceinline__ void from_full(const unsigned* f) {
 #pragma unroll
-    for (int h = 0; h < KPL / 2; ++h) {
-      const unsigned a = v[2 * h] > 0x7fffu ? 0x7fffu : v[2 * h];
-      const unsigned b = v[2 * h + 1] > 0x7fffu ? 0x7fffu : v[2 * h + 1];
-      pv[h] = a | (b << 16);
-    }
+    for (int h = 0; h < KPL / 2; ++h) pv[h] = pk_min_u16(__builtin_amdgcn_perm(f[2 * h + 1], f[2 * h], 0x07060302u), 0x7fff7fffu);
   }
-  // #keys <= x (x <= 0x7fff; real key prefixes are <= 0x7f80, the sign bit is 0): per field
-  // (x + 0x8000) - a keeps bit 15 iff a <= x, with no borrow across fields; popcount on VALU,
-  // one DPP wave sum (no SGPR per compare, no SALU).
+  // #elements <= x (x <= 0x7fff): per field (x + 0x8000) - a keeps bit 15 iff a <= x, with no
+  // borrow across fields; popcount on VALU, one DPP wave sum (no SGPR per compare, no SALU).
   __device__ __forceinline__ int count_le(unsigned x) const {
     const unsigned X2 = (x + 0x8000u) * 0x10001u;
     unsigned c = 0;
@@ -255,26 +246,33 @@ struct Line {
     for (int h = 0; h < KPL / 2; ++h) c = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c;
     return wave_sum((int)c);
   }
+  // min over elements (kNone is above every real prefix) and max over real elements
+  // (kNone + 1 wraps to 0x8000, masked to 0: below every real prefix + 1)
   __device__ __forceinline__ void min_max(unsigned* mn, unsigned* mx) const {
-    unsigned a = 0xffffu, b = 0u;
+    unsigned a = 0xffffffffu, b = 0u;
 #pragma unroll
-    for (int q = 0; q < KPL; ++q) {
-      const bool ok = v[q] != 0xffffffffu;
-      a = ok ? min(a, v[q]) : a;
-      b = ok ? max(b, v[q]) : b;
+    for (int h = 0; h < KPL / 2; ++h) {
+      a = pk_min_u16(a, pv[h]);
+      b = pk_max_u16(b, pk_add_u16(pv[h], 0x00010001u) & 0x7fff7fffu);
     }
+    a = min(a & 0xffffu, a >> 16);
+    b = max(b & 0xffffu, b >> 16);
     *mn = wave_min_u32(a);
-    *mx = wave_max_u32(b);
+    const unsigned m = wave_max_u32(b);
+    *mx = m ? m - 1 : 0u;
   }
   __device__ __forceinline__ unsigned min_greater(unsigned x) const {
     unsigned a = 0xffffffffu;
 #pragma unroll
-    for (int q = 0; q < KPL; ++q) a = (v[q] > x) ? min(a, v[q]) : a;
+    for (int q = 0; q < KPL; ++q) {
+      const unsigned k = pfx(q);
+      a = (k > x && k != kNone) ? min(a, k) : a;
+    }
     return wave_min_u32(a);
   }
 };
 
-// A line of FULL keys (CRP row from F): v = 16-bit prefixes for the search, f = exact keys.
+// A line of FULL keys (CRP row from F): f = exact keys, packed prefixes for the search.
 template <int KPL>
 struct LineFull : Line<KPL> {
   unsigned f[KPL];
@@ -294,9 +292,7 @@ struct LineFull : Line<KPL> {
 #pragma unroll
       for (int q = 0; q < KPL; ++q) f[q] = (base + q < n) ? src[base + q] : 0xffffffffu;
     }
-#pragma unroll
-    for (int q = 0; q < KPL; ++q) this->v[q] = f[q] == 0xffffffffu ? 0xffffffffu : f[q] >> 16;
-    this->pack();
+    this->from_full(f);
   }
 };
 
@@ -334,7 +330,7 @@ __device__ Group group_keys(const Line<KPL>& L, unsigned P, int g, const KF& key
   int base = 0;
 #pragma unroll
   for (int q = 0; q < KPL; ++q) {
-    const bool m = L.v[q] == P;
+    const bool m = L.pfx(q) == P;
     const unsigned long long bal = __ballot(m);
     if (m)
       W.list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] =
@@ -358,7 +354,7 @@ __device__ Group group_keys_full(const LineFull<KPL>& L, unsigned P, int g, Wave
   int base = 0;
 #pragma unroll
   for (int q = 0; q < KPL; ++q) {
-    const bool m = L.v[q] == P;
+    const bool m = L.pfx(q) == P;
     const unsigned long long bal = __ballot(m);
     if (m)
       W.list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] =
@@ -398,7 +394,7 @@ __device__ unsigned big_group_rank(const Line<KPL>& L, unsigned P, int rho, cons
 #pragma unroll
   for (int q = 0; q < KPL; ++q) lw[q] = 0x10000u;
   for (int q = 0; q < KPL; ++q)
-    if (L.v[q] == P) lw[q] = keyf(base + q) & 0xffffu;
+    if (L.pfx(q) == P) lw[q] = keyf(base + q) & 0xffffu;
   unsigned a = 0, b = 0xffffu;
   while (a < b) {
     const unsigned mid = (a + b) >> 1;
@@ -470,7 +466,7 @@ __device__ unsigned row_rank(const LineFull<KPL>& L, unsigned P, int rho, int g,
     const unsigned mid = (a + b) >> 1;
     int c = 0;
 #pragma unroll
-    for (int q = 0; q < KPL; ++q) c += __popcll(__ballot(L.v[q] == P && (L.f[q] & 0xffffu) <= mid));
+    for (int q = 0; q < KPL; ++q) c += __popcll(__ballot(L.pfx(q) == P && (L.f[q] & 0xffffu) <= mid));
     if (c > rho)
       b = mid;
     else
@@ -525,7 +521,7 @@ __device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, 
   int amb = 0;
 #pragma unroll
   for (int q = 0; q < KPL; ++q) {
-    const unsigned k = L.v[q];  // 0xffffffff (no element) is never <= T16
+    const unsigned k = L.pfx(q);  // kNone is never <= T16 (T16 <= 0x7f80)
     word |= (uint32_t)(k < T16) << q;
     amb += k == T16;
   }
@@ -547,7 +543,7 @@ __device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, 
   }
   const int base = lane * KPL;
   for (int q = 0; q < KPL; ++q)
-    if (L.v[q] == T16) word |= (uint32_t)(keyf(base + q) <= Tbits) << q;
+    if (L.pfx(q) == T16) word |= (uint32_t)(keyf(base + q) <= Tbits) << q;
   return word;
 }
 
