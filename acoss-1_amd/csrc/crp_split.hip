@@ -79,21 +79,37 @@ struct KeyPlanes {
 
 constexpr int kTP = 34;  // tile pitch in halfwords: 17 words, odd -> lane stride hits distinct banks
 
-__global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride) {
-  __shared__ __attribute__((aligned(16))) float Ys[kSYRows * 12];
-  __shared__ float Ns[kSCols];
-  __shared__ __attribute__((aligned(16))) uint16_t tileT[kSCols * kTP];  // [column][row] 16-bit prefixes
-  const int p = blockIdx.y;
-  const PairView V = pair_view(B, p);
-  const int strip = blockIdx.x, i0 = strip * kSR;
-  if (i0 >= V.Mp || V.Np <= 0) return;
+// FAST: tau == 1, a full 32-row strip and all 40 query frames inside the track, so the query
+// frames and row norms sit at compile-time offsets from one base (s_load immediates) and no
+// per-row clamp or bound is needed; otherwise the clamped general path.
+template <bool FAST>
+__device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr, int ldc,
+                                           int64_t kstride, float* Ys, float* Ns, uint16_t* tileT) {
+  const int i0 = strip * kSR;
   const int t = threadIdx.x;
-  const int rows = min(kSR, V.Mp - i0);
-  float nq_r[kSR];
-#pragma unroll
-  for (int r = 0; r < kSR; ++r) nq_r[r] = *(const __attribute__((address_space(4))) float*)(V.NXq + min(i0 + r, V.Mp - 1));
+  const int rows = FAST ? kSR : min(kSR, V.Mp - i0);
+  const float* Xi0 = V.X + (size_t)i0 * 12;
+  const float* Nq0 = V.NXq + i0;
+  auto nqr = [&](int r) {  // row norm: a scalar load at a compile-time offset
+    const float* base = Nq0;
+    asm volatile("" : "+s"(base));
+    return *(const __attribute__((address_space(4))) float*)(FAST ? base + r : V.NXq + min(i0 + r, V.Mp - 1));
+  };
   uint32_t* Fr = K.fr + (size_t)p * kstride + (size_t)i0 * ldr;
   uint16_t* Hc = K.hc + (size_t)p * kstride;
+  auto query = [&](int kk, float (&x)[12]) {
+    if (FAST) {
+      const float* base = Xi0;
+      asm volatile("" : "+s"(base));  // keep each row's scalar load in the loop
+      const cfloat4* q = (const cfloat4*)(base + kk * 12);
+      const f32x4 a = q[0], b = q[1], c = q[2];
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+      x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+      x[8] = c.x; x[9] = c.y; x[10] = c.z; x[11] = c.w;
+    } else {
+      load_query(V.X, min((i0 + kk) * V.tau, V.nq - 1), x);
+    }
+  };
   for (int j0 = -(kSR - 1); j0 < V.Np; j0 += kSW) {
     __syncthreads();
     for (int e = t; e < kSYRows * 3; e += kSW) {
@@ -112,7 +128,8 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
     float gw[kMS];
     float xb[2][12];
     f32x4 yb[2][3];
-    load_query(V.X, min(i0 * V.tau, V.nq - 1), xb[0]);
+    query(0, xb[0]);
+    uint32_t* frow = Fr;
     {
       const f32x4* yp = reinterpret_cast<const f32x4*>(Ys + t * 12);
       yb[0][0] = yp[0];
@@ -123,7 +140,7 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
     for (int kk = 0; kk < kSR + kMS - 1; ++kk) {
       const int cur = kk & 1, nxt = cur ^ 1;
       if (kk + 1 < kSR + kMS - 1) {
-        load_query(V.X, min((i0 + kk + 1) * V.tau, V.nq - 1), xb[nxt]);
+        query(kk + 1, xb[nxt]);
         const f32x4* yp = reinterpret_cast<const f32x4*>(Ys + (t + kk + 1) * 12);
         yb[nxt][0] = yp[0];
         yb[nxt][1] = yp[1];
@@ -150,11 +167,15 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
         float dot = 0.0f;
 #pragma unroll
         for (int u = 0; u < kMS; ++u) dot = dot + gw[(r + u) % kMS];
-        const float d2 = (nq_r[r] - 2.0f * dot) + Ns[t + r];
+        const float d2 = (nqr(r) - 2.0f * dot) + Ns[t + r];
         const unsigned key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
         // full key row-major straight from registers: the 64 lanes write 64 consecutive columns
         const int col = j0 + t + r;
-        if (r < rows && col >= 0 && col < V.Np) Fr[(size_t)r * ldr + col] = key;
+        // out-of-range columns (< 0 or >= Np) land in the pad column ldr - 1 (never read):
+        // branchless, no per-row lane masks to keep live
+        if (FAST || r < rows) frow[min((unsigned)col, (unsigned)(ldr - 1))] = key;
+        frow += ldr;  // next row: one scalar add instead of 32 hoisted row pointers
+        asm volatile("" : "+s"(frow));
         tileT[(t + r) * kTP + r] = (uint16_t)(key >> 16);
       }
     }
@@ -181,6 +202,20 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
       reinterpret_cast<uint32_t*>(tileT)[c * (kTP / 2) + w] = reinterpret_cast<const uint32_t*>(tileT)[(kSW + c) * (kTP / 2) + w];
     }
   }
+}
+
+__global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride) {
+  __shared__ __attribute__((aligned(16))) float Ys[kSYRows * 12];
+  __shared__ float Ns[kSCols];
+  __shared__ __attribute__((aligned(16))) uint16_t tileT[kSCols * kTP];  // [column][row] 16-bit prefixes
+  const int p = blockIdx.y;
+  const PairView V = pair_view(B, p);
+  const int strip = blockIdx.x, i0 = strip * kSR;
+  if (i0 >= V.Mp || V.Np <= 0) return;
+  if (V.tau == 1 && i0 + kSR <= V.Mp && i0 + kSR + kMS - 1 <= V.nq)
+    sweep_body<true>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
+  else
+    sweep_body<false>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -289,8 +324,12 @@ struct LineFull : Line<KPL> {
         f[4 * q + 3] = w.w;
       }
     } else {
+      // opaque per-lane count: keeps the 32 tail predicates from being hoisted out of the
+      // caller's row loop into (spilled) SGPR masks
+      int nv = n - base;
+      asm volatile("" : "+v"(nv));
 #pragma unroll
-      for (int q = 0; q < KPL; ++q) f[q] = (base + q < n) ? src[base + q] : 0xffffffffu;
+      for (int q = 0; q < KPL; ++q) f[q] = (q < nv) ? src[base + q] : 0xffffffffu;
     }
     this->from_full(f);
   }
