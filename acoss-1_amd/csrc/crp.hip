@@ -796,7 +796,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   // the row-threshold words RT
   const size_t sub_pair = 6 * (size_t)kstride + 4 * (size_t)mask_stride;
   if (split) {
-    size_t kbudget = (size_t)2 << 30;  // ~80 pairs at 2000 frames: enough blocks to fill 256 CUs
+    size_t kbudget = (size_t)1 << 30;  // ~42 pairs at 2000 frames (x2 buffers): fills 256 CUs per launch
     if (const char* e = getenv("ACOSS_KEY_BYTES")) kbudget = strtoull(e, nullptr, 10);
     sub = (int64_t)(kbudget / sub_pair);
     if (sub < 1) sub = 1;
