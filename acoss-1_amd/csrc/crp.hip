@@ -784,7 +784,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   // Infinity Cache.
   const size_t slot = 4 + 8 + 4 * (size_t)thr_stride * 4 + 4 * (size_t)mask_stride + 16 * (size_t)bnd_stride +
                       4 * (size_t)yrot_stride;
-  size_t budget = (size_t)2 << 30;
+  size_t budget = (size_t)8 << 30;  // DP batch scratch: ~13k pairs at 2000 frames in one DP launch
   if (const char* e = getenv("ACOSS_WS_BYTES")) budget = strtoull(e, nullptr, 10);
   int64_t nbmax = (int64_t)(budget / slot);
   if (const char* e = getenv("ACOSS_BATCH_PAIRS")) nbmax = atoll(e);
