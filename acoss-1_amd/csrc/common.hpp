@@ -114,6 +114,14 @@ __device__ inline double wave_max(double v) {
 // Value of lane `src` (wave-uniform) in every lane: v_readlane, no LDS.
 __device__ __forceinline__ int lane_bcast(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
 
+// XCD-aware block swizzle (speed only, never correctness): blocks are dealt round-robin over
+// the 8 XCDs, so linear ids b and b + 8 share an L2. This bijection on [0, nwg) makes runs of
+// consecutive LOGICAL ids share one XCD (MI355X_MICROARCH.md, workgroup dispatch / T1).
+__device__ __forceinline__ int xcd_remap(int lin, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = lin % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + lin / 8;
+}
+
 // Correctly rounded sqrt (hipcc default: -fhip-fp32-correctly-rounded-divide-sqrt).
 __device__ inline float sqrt_rn(float x) { return __builtin_sqrtf(x); }
 

@@ -646,9 +646,11 @@ __global__ __launch_bounds__(256) void k_sel_cols9(CrpBatch B, KeyPlanes K, int 
                                                    uint32_t* __restrict__ maskT, int64_t mask_stride, int ld) {
   constexpr int KPL = 32;
   __shared__ WaveLds wl[4];
-  const int p = blockIdx.y;
+  // neighbouring columns share the lines of RT and of the F gathers: keep them on one XCD
+  const int lb = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int p = lb / gridDim.x;
   const PairView V = pair_view(B, p);
-  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int j = (lb - p * gridDim.x) * 4 + (threadIdx.x >> 6);
   if (j >= V.Np) return;
   WaveLds& W = wl[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
