@@ -68,8 +68,12 @@ def all_gather_stripes(blk, bounds, group=None):
     import torch.distributed as dist
     n = blk.shape[1]
     rmax = max(r1 - r0 for r0, r1 in bounds)
-    pad = torch.zeros((rmax, n), dtype=blk.dtype, device=blk.device)
-    pad[: blk.shape[0]] = blk
+    # gloo collectives take host tensors: route a device block through host memory
+    host = dist.get_backend(group) == "gloo" and blk.is_cuda
+    src = blk.cpu() if host else blk
+    pad = torch.zeros((rmax, n), dtype=src.dtype, device=src.device)
+    pad[: src.shape[0]] = src
     outs = [torch.empty_like(pad) for _ in bounds]
     dist.all_gather(outs, pad, group=group)
-    return torch.cat([o[: r1 - r0] for o, (r0, r1) in zip(outs, bounds)], 0)
+    full = torch.cat([o[: r1 - r0] for o, (r0, r1) in zip(outs, bounds)], 0)
+    return full.to(blk.device) if host else full
