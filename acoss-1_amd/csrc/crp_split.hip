@@ -19,6 +19,7 @@
 //                holds rows 32l..32l+31 of the column, i.e. exactly one 32-bit CRP word:
 //                (key <= T_col bits) & RT[strip l][j].
 #include <cstdlib>
+#include <cstring>
 
 #include "crp_internal.hpp"
 
@@ -592,21 +593,18 @@ __device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, 
 // ---------------------------------------------------------------------------------------
 constexpr int kRowWaves = 8;
 
-__global__ __launch_bounds__(512, 4) void k_sel_rows9(CrpBatch B, KeyPlanes K, int ldr, int64_t kstride, float kappa,
-                                                   float* __restrict__ thr, float* __restrict__ Tq,
-                                                   int64_t thr_stride, uint32_t* __restrict__ RT,
-                                                   int64_t rt_stride, int ld) {
+// Row select of one (32-row strip, pair) by NW waves: wave w takes rows w, w+NW, ...
+template <int NW>
+__device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr,
+                                          int64_t kstride, float kappa, float* __restrict__ thr,
+                                          float* __restrict__ Tq, int64_t thr_stride, uint32_t* __restrict__ RT,
+                                          int64_t rt_stride, int ld, WaveLds* wl, uint32_t (*rowbits)[64]) {
   constexpr int KPL = 32;
-  __shared__ WaveLds wl[kRowWaves];
-  __shared__ uint32_t rowbits[kSR][64];
-  const int p = blockIdx.y;
-  const PairView V = pair_view(B, p);
-  const int strip = blockIdx.x, i0 = strip * kSR;
-  if (i0 >= V.Mp) return;
+  const int i0 = strip * kSR;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   WaveLds& W = wl[w];
 #pragma unroll 1
-  for (int r = w; r < kSR; r += kRowWaves) {
+  for (int r = w; r < kSR; r += NW) {
     const int i = i0 + r;
     uint32_t word = 0;
     if (i < V.Mp) {
@@ -627,13 +625,54 @@ __global__ __launch_bounds__(512, 4) void k_sel_rows9(CrpBatch B, KeyPlanes K, i
   __syncthreads();
   // transpose: word of column j = bit (j & 31) of rowbits[r][j >> 5], r = 0..31
   uint32_t* out = RT + (size_t)p * rt_stride + (size_t)strip * ld;
-  for (int j = threadIdx.x; j < V.Np; j += 512) {
+  for (int j = threadIdx.x; j < V.Np; j += NW * 64) {
     const int l = j >> 5, q = j & 31;
     uint32_t word = 0;
 #pragma unroll
     for (int r = 0; r < kSR; ++r) word |= ((rowbits[r][l] >> q) & 1u) << r;
     out[j] = word;
   }
+}
+
+__global__ __launch_bounds__(512, 4) void k_sel_rows9(CrpBatch B, KeyPlanes K, int ldr, int64_t kstride, float kappa,
+                                                   float* __restrict__ thr, float* __restrict__ Tq,
+                                                   int64_t thr_stride, uint32_t* __restrict__ RT,
+                                                   int64_t rt_stride, int ld) {
+  __shared__ WaveLds wl[kRowWaves];
+  __shared__ uint32_t rowbits[kSR][64];
+  const int p = blockIdx.y;
+  const PairView V = pair_view(B, p);
+  const int strip = blockIdx.x;
+  if (strip * kSR >= V.Mp) return;
+  rows_body<kRowWaves>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+}
+
+// Sweep and row select fused: the block selects the 32 rows it has just swept, reading its
+// full keys back while they are cache-resident (no second pass over F from HBM, one launch
+// fewer). LDS of the two phases is one union.
+constexpr int kSweepLds = (kSYRows * 12 + kSCols) * 4 + kSCols * kTP * 2;
+constexpr int kRowsLds = 4 * (int)sizeof(WaveLds) + kSR * 64 * 4;
+constexpr int kFusedLds = kSweepLds > kRowsLds ? kSweepLds : kRowsLds;
+
+__global__ __launch_bounds__(256, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride,
+                                                     float kappa, float* __restrict__ thr, float* __restrict__ Tq,
+                                                     int64_t thr_stride, uint32_t* __restrict__ RT, int64_t rt_stride,
+                                                     int ld) {
+  __shared__ __attribute__((aligned(16))) char smem[kFusedLds];
+  float* Ys = reinterpret_cast<float*>(smem);
+  float* Ns = Ys + kSYRows * 12;
+  uint16_t* tileT = reinterpret_cast<uint16_t*>(Ns + kSCols);
+  const int p = blockIdx.y;
+  const PairView V = pair_view(B, p);
+  const int strip = blockIdx.x, i0 = strip * kSR;
+  if (i0 >= V.Mp || V.Np <= 0) return;
+  if (V.tau == 1 && i0 + kSR <= V.Mp && i0 + kSR + kMS - 1 <= V.nq)
+    sweep_body<true>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
+  else
+    sweep_body<false>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
+  __syncthreads();  // the strip's F rows are complete (block-scope visibility of the global stores)
+  rows_body<4>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld,
+               reinterpret_cast<WaveLds*>(smem), reinterpret_cast<uint32_t(*)[64]>(smem + 4 * sizeof(WaveLds)));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -684,15 +723,27 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
   const size_t plane = (size_t)nb * kstride;
   const KeyPlanes K{static_cast<uint32_t*>(kplanes), reinterpret_cast<uint16_t*>(static_cast<uint32_t*>(kplanes) + plane)};
   const int nstrips = (L + kSR - 1) / kSR;
-  prof_begin(PH_SWEEP, s);
-  hipLaunchKernelGGL(k_sweep9, dim3(nstrips, nb), dim3(kSW), 0, s, B, K, ldk, ldk, kstride);
-  ACOSS_LAUNCH_CHECK();
-  prof_end(PH_SWEEP, s);
-  prof_begin(PH_SEL_ROWS, s);
-  hipLaunchKernelGGL(k_sel_rows9, dim3(nstrips, nb), dim3(512), 0, s, B, K, ldk, kstride, kappa, thr_r, T_r,
-                     thr_stride, RT, mask_stride, ld);
-  ACOSS_LAUNCH_CHECK();
-  prof_end(PH_SEL_ROWS, s);
+  static const bool fused = [] {
+    const char* e = getenv("ACOSS_FUSE_ROWS");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  if (fused) {
+    prof_begin(PH_SWEEP, s);
+    hipLaunchKernelGGL(k_sweep_rows9, dim3(nstrips, nb), dim3(256), 0, s, B, K, ldk, ldk, kstride, kappa, thr_r, T_r,
+                       thr_stride, RT, mask_stride, ld);
+    ACOSS_LAUNCH_CHECK();
+    prof_end(PH_SWEEP, s);
+  } else {
+    prof_begin(PH_SWEEP, s);
+    hipLaunchKernelGGL(k_sweep9, dim3(nstrips, nb), dim3(kSW), 0, s, B, K, ldk, ldk, kstride);
+    ACOSS_LAUNCH_CHECK();
+    prof_end(PH_SWEEP, s);
+    prof_begin(PH_SEL_ROWS, s);
+    hipLaunchKernelGGL(k_sel_rows9, dim3(nstrips, nb), dim3(512), 0, s, B, K, ldk, kstride, kappa, thr_r, T_r,
+                       thr_stride, RT, mask_stride, ld);
+    ACOSS_LAUNCH_CHECK();
+    prof_end(PH_SEL_ROWS, s);
+  }
   prof_begin(PH_SEL_COLS, s);
   hipLaunchKernelGGL(k_sel_cols9, dim3((L + 3) / 4, nb), dim3(256), 0, s, B, K, ldk, kstride, kappa, RT, thr_c, T_c,
                      thr_stride, maskT, mask_stride, ld);
