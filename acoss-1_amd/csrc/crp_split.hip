@@ -336,16 +336,50 @@ struct LineFull : Line<KPL> {
   }
 };
 
-// Smallest prefix P with count(keys <= P) > rho.
+// Smallest prefix P with count(keys <= P) > rho, bisecting [a, b]; also returns
+// le = count(<= P) and less = count(< P) (carried through the search: no extra counts).
+// hint (wave-uniform, or kNoHint): the previous line's answer. Adjacent stacked rows/columns
+// share 8 of their 9 frames, so the answer is usually a few prefixes away: gallop out from
+// the hint to a bracket, then bisect inside it.
+constexpr unsigned kNoHint = 0xffffffffu;
+
 template <int KPL>
-__device__ __forceinline__ unsigned prefix_of_rank(const Line<KPL>& L, int rho, unsigned a, unsigned b) {
+__device__ __forceinline__ unsigned prefix_of_rank(const Line<KPL>& L, int rho, unsigned a, unsigned b, int n,
+                                                   unsigned hint, int* le_out, int* less_out) {
+  int c_b = n;    // count(<= b): every element is <= kmax
+  int c_am1 = 0;  // count(<= a - 1): none is below kmin
+  // one count per iteration, probe chosen by the mode (a single count_le site keeps the
+  // unrolled SWAR body once): 0 hint, 1 gallop down, 2 gallop up, 3 bisect
+  int mode = (hint != kNoHint) ? 0 : 3;
+  unsigned step = 1;
   while (a < b) {
-    const unsigned mid = (a + b) >> 1;
-    if (L.count_le(mid) > rho)
-      b = mid;
+    unsigned t;
+    if (mode == 0)
+      t = hint < a ? a : (hint > b ? b : hint);
+    else if (mode == 1)
+      t = (b - a > step) ? b - step : a;
+    else if (mode == 2)
+      t = (b - a > step) ? a + step - 1 : (a + b) >> 1;
     else
-      a = mid + 1;
+      t = (a + b) >> 1;
+    const int c = L.count_le(t);
+    const bool greater = c > rho;
+    if (greater) {
+      b = t;
+      c_b = c;
+    } else {
+      a = t + 1;
+      c_am1 = c;
+    }
+    if (mode == 0)
+      mode = greater ? 1 : 2;
+    else if (mode == 1)
+      mode = greater ? (step <<= 1, 1) : 3;
+    else if (mode == 2)
+      mode = greater ? 3 : (step <<= 1, 2);
   }
+  *le_out = c_b;
+  *less_out = c_am1;
   return a;
 }
 
@@ -463,15 +497,15 @@ __device__ unsigned rank_in_prefix(const Line<KPL>& L, unsigned P, int rho, int 
 // exact keys of the last batched group in *cache for le_bits.
 template <int KPL, class KF>
 __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF& keyf, WaveLds& W, Group* c_lo,
-                               Group* c_hi, float* thr, float* T) {
+                               Group* c_hi, float* thr, float* T, unsigned* hint) {
   const float q = (float)(n - 1) * kappa;
   const float lo_f = floorf(q), hi_f = ceilf(q);
   const int lo = (int)lo_f, hi = (int)hi_f;
   unsigned kmin, kmax;
   L.min_max(&kmin, &kmax);
-  const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax);
-  const int le = L.count_le(Pl);
-  const int less = Pl > kmin ? L.count_le(Pl - 1) : 0;
+  int le, less;
+  const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, *hint, &le, &less);
+  *hint = Pl;
   const unsigned vlo = rank_in_prefix(L, Pl, lo - less, le - less, keyf, W, c_lo);
   unsigned vhi = vlo;
   if (hi != lo) {
@@ -516,15 +550,16 @@ __device__ unsigned row_rank(const LineFull<KPL>& L, unsigned P, int rho, int g,
 }
 
 template <int KPL>
-__device__ void row_threshold(const LineFull<KPL>& L, int n, float kappa, WaveLds& W, float* thr, float* T) {
+__device__ void row_threshold(const LineFull<KPL>& L, int n, float kappa, WaveLds& W, float* thr, float* T,
+                              unsigned* hint) {
   const float q = (float)(n - 1) * kappa;
   const float lo_f = floorf(q), hi_f = ceilf(q);
   const int lo = (int)lo_f, hi = (int)hi_f;
   unsigned kmin, kmax;
   L.min_max(&kmin, &kmax);
-  const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax);
-  const int le = L.count_le(Pl);
-  const int less = Pl > kmin ? L.count_le(Pl - 1) : 0;
+  int le, less;
+  const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, *hint, &le, &less);
+  *hint = Pl;
   const unsigned vlo = row_rank(L, Pl, lo - less, le - less, W);
   unsigned vhi = vlo;
   if (hi != lo) {
@@ -603,15 +638,17 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
   const int i0 = strip * kSR;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   WaveLds& W = wl[w];
+  constexpr int RPW = kSR / NW;  // consecutive rows per wave: each search starts from its neighbour's
+  unsigned hint = kNoHint;
 #pragma unroll 1
-  for (int r = w; r < kSR; r += NW) {
+  for (int r = w * RPW; r < (w + 1) * RPW; ++r) {
     const int i = i0 + r;
     uint32_t word = 0;
     if (i < V.Mp) {
       LineFull<KPL> L;
       L.load_full(K.fr + (size_t)p * kstride + (size_t)i * ldr, V.Np);
       float th, T;
-      row_threshold(L, V.Np, kappa, W, &th, &T);
+      row_threshold(L, V.Np, kappa, W, &th, &T, &hint);
       if (lane == 0) {
         thr[(size_t)p * thr_stride + i] = th;
         Tq[(size_t)p * thr_stride + i] = T;
@@ -700,7 +737,8 @@ __global__ __launch_bounds__(256) void k_sel_cols9(CrpBatch B, KeyPlanes K, int 
   float th, Tc;
   Group c_lo, c_hi;
   c_lo.g = c_hi.g = -1;
-  line_threshold(L, V.Mp, kappa, keyf, W, &c_lo, &c_hi, &th, &Tc);
+  unsigned hint = kNoHint;
+  line_threshold(L, V.Mp, kappa, keyf, W, &c_lo, &c_hi, &th, &Tc, &hint);
   if (lane == 0) {
     thr[(size_t)p * thr_stride + j] = th;
     Tq[(size_t)p * thr_stride + j] = Tc;
