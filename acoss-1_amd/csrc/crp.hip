@@ -429,15 +429,16 @@ __global__ __launch_bounds__(256) void k_crp_panel(CrpBatch B, const float* __re
 }
 
 // --------------------------------------------------------------------------------------
-// k_crp_dp<ALIGN, EQG>: essentia CoverSongSimilarity(serra09 | chen17, 'symmetric').
-// One wave per pair; lane l owns rows band*2048 + 32l .. +31; column c = s - l at step s.
+// k_crp_dp<ALIGN, EQG, R>: essentia CoverSongSimilarity(serra09 | chen17, 'symmetric').
+// One wave per pair; lane l owns R rows, band*64R + Rl .. +R-1 (R = 32, 16 or 8 by the batch's
+// longest CRP, so short tracks keep every lane busy); column c = s - l at step s.
 // --------------------------------------------------------------------------------------
 struct DpAbove {  // what lane l-1 (or the band above) hands down for one column
-  float q30, q31;
-  uint32_t b;     // bit0 = C[row 30], bit1 = C[row 31]
+  float q30, q31;  // its last two rows (R-2, R-1)
+  uint32_t b;      // bit0 = C[row R-2], bit1 = C[row R-1]
 };
 
-template <int ALIGN, bool EQG>
+template <int ALIGN, bool EQG, int R>
 struct DpLane {
   float go, ge;
   int Np, lane, c_off;  // column of this lane at step s: s - lane
@@ -450,7 +451,7 @@ struct DpLane {
 
   // qn: new column c; q1: column c-1; q2: column c-2. w0: CRP word of column c;
   // h0: from above for column c. Returns the values to hand to the lane below.
-  __device__ __forceinline__ DpAbove step(float (&qn)[32], const float (&q1)[32], const float (&q2)[32],
+  __device__ __forceinline__ DpAbove step(float (&qn)[R], const float (&q1)[R], const float (&q2)[R],
                                           uint32_t w0, const DpAbove& h0, int c) {
     const bool colvalid = (c >= 2) && (c < Np);
     const uint32_t vmask = colvalid ? rowvalid : 0u;
@@ -459,7 +460,7 @@ struct DpLane {
     const uint64_t e1 = ((uint64_t)w1 << 2) | h1.b;
     const uint64_t e2 = ((uint64_t)w2 << 2) | h2.b;
 #pragma unroll
-    for (int r = 0; r < 32; ++r) {
+    for (int r = 0; r < R; ++r) {
       const float Qa = r >= 1 ? q1[r - 1] : h1.q31;                            // Q[r-1][c-1]
       float Qb = r >= 2 ? q1[r - 2] : (r == 1 ? h1.q31 : h1.q30);              // Q[r-2][c-1]
       float Qc = r >= 1 ? q2[r - 1] : h2.q31;                                  // Q[r-1][c-2]
@@ -484,9 +485,9 @@ struct DpLane {
       qn[r] = v;
     }
     DpAbove out;
-    out.q30 = qn[30];
-    out.q31 = qn[31];
-    out.b = (w0 >> 30) & 3u;
+    out.q30 = qn[R - 2];
+    out.q31 = qn[R - 1];
+    out.b = (w0 >> (R - 2)) & 3u;
     h2 = h1;
     h1 = h0;
     w2 = w1;
@@ -495,7 +496,7 @@ struct DpLane {
   }
 };
 
-template <int ALIGN, bool EQG>
+template <int ALIGN, bool EQG, int R>
 __global__ __launch_bounds__(64) void k_crp_dp(const uint32_t* __restrict__ maskT, int64_t mask_stride, int ld,
                                                const int2* __restrict__ dims, float go, float ge,
                                                float4* __restrict__ bnd, int64_t bnd_stride,
@@ -505,30 +506,36 @@ __global__ __launch_bounds__(64) void k_crp_dp(const uint32_t* __restrict__ mask
   const int2 dm = dims[p];
   const int Mp = dm.x, Np = dm.y;
   float best = 0.0f;
-  const int nbands = (Mp + 2047) / 2048;
+  constexpr int kBand = 64 * R;
+  const int nbands = (Mp + kBand - 1) / kBand;
   for (int band = 0; band < nbands; ++band) {
-    const uint32_t* mrow = maskT + (size_t)p * mask_stride + (size_t)(band * 64 + lane) * ld;
+    const int row0 = band * kBand + lane * R;
+    const uint32_t* mrow = maskT + (size_t)p * mask_stride + (size_t)(row0 >> 5) * ld;
+    const int sh = row0 & 31;  // this lane's R rows inside its 32-row strip word
     float4* bout = bnd + (size_t)p * bnd_stride + (size_t)band * ld;
     const float4* bin = bnd + (size_t)p * bnd_stride + (size_t)(band - 1) * ld;
-    DpLane<ALIGN, EQG> L;
+    DpLane<ALIGN, EQG, R> L;
     L.go = go;
     L.ge = ge;
     L.Np = Np;
     L.lane = lane;
-    const int row0 = band * 2048 + lane * 32;
     uint32_t rv = 0;
-    for (int r = 0; r < 32; ++r) rv |= (uint32_t)((row0 + r >= 2) && (row0 + r < Mp)) << r;
+    for (int r = 0; r < R; ++r) rv |= (uint32_t)((row0 + r >= 2) && (row0 + r < Mp)) << r;
     L.rowvalid = rv;
     L.w1 = L.w2 = 0;
     L.h1 = L.h2 = DpAbove{0.0f, 0.0f, 0u};
     L.best = 0.0f;
-    float qa[32], qb[32], qc[32];
+    float qa[R], qb[R], qc[R];
 #pragma unroll
-    for (int r = 0; r < 32; ++r) qa[r] = qb[r] = qc[r] = 0.0f;
+    for (int r = 0; r < R; ++r) qa[r] = qb[r] = qc[r] = 0.0f;
     DpAbove pub{0.0f, 0.0f, 0u};
     const int S_end = Np + 63;
     const bool lane_active = row0 < Mp;
-    auto fetch = [&](int c) -> uint32_t { return (lane_active && c >= 0 && c < Np) ? mrow[c] : 0u; };
+    auto fetch = [&](int c) -> uint32_t {
+      if (!(lane_active && c >= 0 && c < Np)) return 0u;
+      const uint32_t w = mrow[c];
+      return R == 32 ? w : (w >> sh) & ((1u << (R & 31)) - 1u);
+    };
     auto recv = [&](const DpAbove& mine, int c) -> DpAbove {
       DpAbove h;
       h.q30 = __shfl_up(mine.q30, 1);
@@ -665,15 +672,28 @@ int prepare_stage(int m, int ld, Stage* st) {
   return ACOSS_OK;
 }
 
-template <int ALIGN>
-void launch_dp(bool eqg, int nb, const uint32_t* maskT, int64_t mstride, int ld, const int2* dims, float go,
-               float ge, float4* bnd, int64_t bstride, float* out, hipStream_t s) {
+template <int ALIGN, int R>
+void launch_dp_r(bool eqg, int nb, const uint32_t* maskT, int64_t mstride, int ld, const int2* dims, float go,
+                 float ge, float4* bnd, int64_t bstride, float* out, hipStream_t s) {
   if (eqg)
-    hipLaunchKernelGGL((k_crp_dp<ALIGN, true>), dim3(nb), dim3(64), 0, s, maskT, mstride, ld, dims, go, ge, bnd,
+    hipLaunchKernelGGL((k_crp_dp<ALIGN, true, R>), dim3(nb), dim3(64), 0, s, maskT, mstride, ld, dims, go, ge, bnd,
                        bstride, out);
   else
-    hipLaunchKernelGGL((k_crp_dp<ALIGN, false>), dim3(nb), dim3(64), 0, s, maskT, mstride, ld, dims, go, ge, bnd,
+    hipLaunchKernelGGL((k_crp_dp<ALIGN, false, R>), dim3(nb), dim3(64), 0, s, maskT, mstride, ld, dims, go, ge, bnd,
                        bstride, out);
+}
+
+// Rows per lane from the batch's longest CRP (L rows): every choice below 2048 rows is one band,
+// so the band-boundary buffer (ceil(L / 2048) bands) always suffices.
+template <int ALIGN>
+void launch_dp(bool eqg, int nb, int L, const uint32_t* maskT, int64_t mstride, int ld, const int2* dims, float go,
+               float ge, float4* bnd, int64_t bstride, float* out, hipStream_t s) {
+  if (L <= 512)
+    launch_dp_r<ALIGN, 8>(eqg, nb, maskT, mstride, ld, dims, go, ge, bnd, bstride, out, s);
+  else if (L <= 1024)
+    launch_dp_r<ALIGN, 16>(eqg, nb, maskT, mstride, ld, dims, go, ge, bnd, bstride, out, s);
+  else
+    launch_dp_r<ALIGN, 32>(eqg, nb, maskT, mstride, ld, dims, go, ge, bnd, bstride, out, s);
 }
 
 // Thresholds of one side: fast m=9 path (crp_select.hip) unless ACOSS_SELECT_GENERIC is set
@@ -891,14 +911,14 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
     }
     if (qmax_out) {
       prof_begin(PH_DP_QMAX, s);
-      launch_dp<0>(eqg, nb, w_mask, mask_stride, ld, w_dims, params->gamma_open, params->gamma_ext, w_bnd,
+      launch_dp<0>(eqg, nb, L, w_mask, mask_stride, ld, w_dims, params->gamma_open, params->gamma_ext, w_bnd,
                    bnd_stride, qmax_out + base, s);
       ACOSS_LAUNCH_CHECK();
       prof_end(PH_DP_QMAX, s);
     }
     if (dmax_out) {
       prof_begin(PH_DP_DMAX, s);
-      launch_dp<1>(eqg, nb, w_mask, mask_stride, ld, w_dims, params->gamma_open, params->gamma_ext, w_bnd,
+      launch_dp<1>(eqg, nb, L, w_mask, mask_stride, ld, w_dims, params->gamma_open, params->gamma_ext, w_bnd,
                    bnd_stride, dmax_out + base, s);
       ACOSS_LAUNCH_CHECK();
       prof_end(PH_DP_DMAX, s);
@@ -1013,9 +1033,9 @@ extern "C" int acoss_align_crp(const uint8_t* crp, int32_t M, int32_t N, int32_t
   ACOSS_LAUNCH_CHECK();
   const bool eqg = gamma_open == gamma_ext;
   if (align == 0)
-    launch_dp<0>(eqg, 1, maskT, 0, ld, d_dims, gamma_open, gamma_ext, bnd, 0, score_out, s);
+    launch_dp<0>(eqg, 1, M, maskT, 0, ld, d_dims, gamma_open, gamma_ext, bnd, 0, score_out, s);
   else
-    launch_dp<1>(eqg, 1, maskT, 0, ld, d_dims, gamma_open, gamma_ext, bnd, 0, score_out, s);
+    launch_dp<1>(eqg, 1, M, maskT, 0, ld, d_dims, gamma_open, gamma_ext, bnd, 0, score_out, s);
   ACOSS_LAUNCH_CHECK();
   int h_err = 0;
   ACOSS_HIP_CHECK(hipMemcpyAsync(&h_err, d_err, 4, hipMemcpyDeviceToHost, s));
