@@ -47,6 +47,8 @@ SIGNATURES = {
     "acoss_simple_mp": [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _vp],
     "acoss_median_downsample": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
     "acoss_simple_features": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _i64, _vp],
+    "acoss_earlyfusion": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, ctypes.c_double,
+                          _i32, _f32, _vp, _vp],
     "acoss_release_workspace": [],
     "acoss_profile_enable": [ctypes.c_int],
     "acoss_profile_read": [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int],
@@ -378,6 +380,27 @@ def simple_features(feats, track_off, track_len, win=200, skip=100, win_len_smoo
                                    w.ctypes.data_as(ctypes.c_void_p), len(w), _ptr(out), _ptr(oo), total, _stream())
     _check(rc, "acoss_simple_features")
     return out[:total], out_off, T.astype(np.int32)
+
+
+def earlyfusion(bank, pairs, kappa=0.1, K=10, mu=0.5):
+    """Batched EarlyFusion scores (earlyfusion_traile.py:157-198). bank: dict of device tensors
+    'mfccs', 'ssms', 'chromas' (sum nb x d, float32), 'chroma_med' (T x 12), 'off' (T,) int64,
+    'nb' (T,) int32 and host 'max_blocks'. Returns (P, 4) float64 device tensor with columns
+    mfccs, ssms, chromas, early."""
+    torch = _torch()
+    lib = load_library()
+    pairs = _dev(pairs, torch.int32).reshape(-1, 2)
+    _check_pairs(pairs, int(bank["nb"].shape[0]))
+    P = pairs.shape[0]
+    out = torch.empty((P, 4), dtype=torch.float64, device="cuda")
+    if P == 0:
+        return out
+    rc = lib.acoss_earlyfusion(_ptr(bank["mfccs"]), _ptr(bank["ssms"]), _ptr(bank["chromas"]), _ptr(bank["chroma_med"]),
+                               _ptr(bank["off"]), _ptr(bank["nb"]), int(bank["nb"].shape[0]), int(bank["max_blocks"]),
+                               int(bank["mfccs"].shape[1]), int(bank["ssms"].shape[1]), int(bank["chromas"].shape[1]),
+                               _ptr(pairs), int(P), float(kappa), int(K), float(mu), _ptr(out), _stream())
+    _check(rc, "acoss_earlyfusion")
+    return out
 
 
 def profile_enable(on=True):

@@ -151,23 +151,37 @@ class EarlyFusion(CoverAlgorithm):
         mats.append(_lib.binarize_rows(torch.exp(-wsum), nn))
         return mats
 
+    def _bank(self):
+        """All tracks' block features packed once into HBM for the batched kernels."""
+        if getattr(self, "_dev_bank", None) is None:
+            torch = _lib._torch()
+            self.prepare()
+            feats = [self.load_features(i) for i in range(self.N)]
+            nb = np.array([f["mfccs"].shape[0] for f in feats], np.int32)
+            off = np.zeros(self.N, np.int64)
+            off[1:] = np.cumsum(nb[:-1])
+
+            def cat(key):
+                return torch.as_tensor(np.ascontiguousarray(np.concatenate([f[key] for f in feats]), np.float32)).cuda()
+
+            self._dev_bank = {"mfccs": cat("mfccs"), "ssms": cat("ssms"), "chromas": cat("chromas"),
+                              "chroma_med": torch.as_tensor(np.stack([np.asarray(f["chroma_med"], np.float32)
+                                                                      for f in feats])).cuda(),
+                              "off": torch.as_tensor(off).cuda(), "nb": torch.as_tensor(nb).cuda(),
+                              "max_blocks": int(nb.max())}
+        return self._dev_bank
+
     def similarity(self, idxs, do_plot=False):
+        """The four scores of every pair, one batched C-ABI call (acoss_earlyfusion)."""
         idxs = np.asarray(idxs)
         if len(idxs) == 0:
             return
-        keys = ("mfccs", "ssms", "chromas", "early")
-        step = 512
-        for c0 in range(0, len(idxs), step):
-            chunk = idxs[c0:c0 + step]
-            tic = time.time()
-            mats = []
-            for i, j in chunk:
-                mats.extend(self.pair_matrices(int(i), int(j)))
-            scores = _lib.sw_constrained(mats).cpu().numpy().reshape(len(chunk), 4)
-            if self.log_times:
-                self.times['raw'].append((time.time() - tic) / len(chunk))
-            for s, key in enumerate(keys):
-                self.Ds[key][chunk[:, 0], chunk[:, 1]] = scores[:, s]
+        tic = time.time()
+        scores = _lib.earlyfusion(self._bank(), idxs.astype(np.int32), self.kappa, self.K).cpu().numpy()
+        if self.log_times:
+            self.times['raw'].append((time.time() - tic) / len(idxs))
+        for s, key in enumerate(("mfccs", "ssms", "chromas", "early")):
+            self.Ds[key][idxs[:, 0], idxs[:, 1]] = scores[:, s]
 
     def prepare(self):
         if not self._prepared:

@@ -1,0 +1,405 @@
+// earlyfusion.hip — EarlyFusion.similarity (acoss/algorithms/earlyfusion_traile.py:157-198) for a
+// batch of pairs: one launch per stage for a whole chunk of pairs instead of ~15 launches per pair.
+//
+// Per pair (a, b) with beat-synchronous block features (M = n_blocks[a] rows, N = n_blocks[b]):
+//   CSM_m = get_csm(mfccs_a, mfccs_b)              euclid, d = 1000   (:173)
+//   CSM_s = get_csm(ssms_a, ssms_b)                euclid, d = 1225   (:175)
+//   CSM_c = get_csm_blocked_oti(chromas_a, chromas_b, med_a, med_b, get_csm_cosine)  d = 480 (:178)
+//   scores[mfccs|ssms|chromas] = SW(csm_to_binary(CSM_x, kappa))                      (:174-181)
+//   W = ((0 + getWCSM(CSM_m)) + getWCSM(CSM_s)) + getWCSM(CSM_c); E = exp(-W)          (:184-188)
+//   scores[early] = SW(csm_to_binary(E, kappa))                                        (:189)
+// Stages (workspace chunk of P pairs, every per-pair matrix padded to ld x ld):
+//   k_ef_rows     per block row: squared norm (euclid) / L2-normalised copy (cosine; zero -> 1)
+//   k_ef_oti      per pair: get_oti(med_a, med_b), first maximum
+//   k_ef_csm<K>   64x64 MFMA f32 tiles x pairs (blockIdx.z); the OTI roll of the query's 12-bin
+//                 blocks is applied in the tile loader
+//   k_ef_binarize wave per (row, pair, matrix): the round(kappa * N) smallest -> 1, ties lowest column
+//   k_ef_kmean    wave per (row|column, pair, matrix): mean of the K smallest
+//   k_ef_wsum     elementwise: E = exp(-(((0 + W_m) + W_s) + W_c)) in float32
+//   SW            launch_sw_batch (misc.hip) over the 4P binary matrices
+// Tolerance vs the reference: the GEMMs' summation order (BLAS vs MFMA); every other step is the
+// reference's float32 arithmetic.
+#include <cmath>
+#include <cstdlib>
+
+#include "common.hpp"
+
+namespace acoss {
+
+int launch_sw_batch(const uint8_t* mats, const int64_t* off, const int32_t* rows, const int32_t* cols,
+                    const int32_t* ldm, int n, int max_rows, int max_cols, void* bnd, double* out, int* err,
+                    hipStream_t s);
+size_t sw_bnd_bytes(int max_rows, int max_cols);
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kT = 64, kKC = 32;
+
+__device__ __forceinline__ unsigned fkey(float f) {
+  const unsigned u = __builtin_bit_cast(unsigned, f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ void k_ef_rows(const float* __restrict__ X, int64_t nrows, int d, int normalise, float* __restrict__ Xo,
+                          float* __restrict__ sq) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= nrows) return;
+  const float* x = X + row * d;
+  float s = 0.0f;
+  for (int c = lane; c < d; c += 64) s += x[c] * x[c];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (!normalise) {
+    if (lane == 0) sq[row] = s;
+    return;
+  }
+  const float nrm = sqrtf(s);
+  const float den = nrm != 0.0f ? nrm : 1.0f;  // XNorm[XNorm == 0] = 1 (cross_recurrence.py:67-70)
+  for (int c = lane; c < d; c += 64) Xo[row * d + c] = x[c] / den;
+}
+
+__global__ void k_ef_oti(const float* __restrict__ med, const int32_t* __restrict__ pairs, int P,
+                         int* __restrict__ oti) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const float* a = med + pairs[2 * p] * 12;
+  const float* b = med + pairs[2 * p + 1] * 12;
+  int best = 0;
+  float bv = 0.0f;
+  for (int i = 0; i < 12; ++i) {
+    float s = 0.0f;
+    for (int c = 0; c < 12; ++c) s = s + a[(c - i + 12) % 12] * b[c];
+    if (i == 0 || s > bv) {
+      bv = s;
+      best = i;
+    }
+  }
+  oti[p] = best;
+}
+
+struct EfPairs {
+  const int32_t* pairs;
+  const int64_t* off;  // block offsets per track
+  const int32_t* nb;   // blocks per track
+};
+
+__device__ __forceinline__ void pair_dims(const EfPairs& E, int p, int* a, int* b, int* M, int* N) {
+  *a = E.pairs[2 * p];
+  *b = E.pairs[2 * p + 1];
+  *M = E.nb[*a];
+  *N = E.nb[*b];
+}
+
+template <int KIND>  // 0 euclid, 1 cosine (pre-normalised rows, query blocks rolled by oti)
+__global__ __launch_bounds__(256) void k_ef_csm(const float* __restrict__ bank, int d, const float* __restrict__ sq,
+                                                EfPairs E, const int* __restrict__ oti, int ld,
+                                                float* __restrict__ out) {
+  __shared__ float Xs[kT][kKC + 1];
+  __shared__ float Ys[kT][kKC + 1];
+  const int p = blockIdx.z;
+  int a, b, M, N;
+  pair_dims(E, p, &a, &b, &M, &N);
+  const int bi = blockIdx.y * kT, bj = blockIdx.x * kT;
+  if (bi >= M || bj >= N) return;
+  const float* X = bank + E.off[a] * d;
+  const float* Y = bank + E.off[b] * d;
+  const int roll = KIND == 1 ? oti[p] : 0;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  f32x16 acc = {};
+  for (int k0 = 0; k0 < d; k0 += kKC) {
+    __syncthreads();
+    for (int e = t; e < kT * kKC; e += 256) {
+      const int r = e / kKC, c = e - r * kKC;
+      const int k = k0 + c;
+      int kx = k;
+      if (KIND == 1 && roll) {  // X1 = np.roll(X blocks, oti, axis=2): X1[k] = X[blk*12 + (cc - oti) mod 12]
+        const int blk = k / 12, cc = k - blk * 12;
+        kx = blk * 12 + (cc - roll + 12) % 12;
+      }
+      Xs[r][c] = (bi + r < M && k < d) ? X[(size_t)(bi + r) * d + kx] : 0.0f;
+      Ys[r][c] = (bj + r < N && k < d) ? Y[(size_t)(bj + r) * d + k] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kKC; kk += 2) {
+      const float xa = Xs[32 * wr + (lane & 31)][kk + (lane >> 5)];
+      const float yb = Ys[32 * wc + (lane & 31)][kk + (lane >> 5)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa, yb, acc, 0, 0, 0);
+    }
+  }
+  float* o = out + (size_t)p * ld * ld;
+  const int col = bj + 32 * wc + (lane & 31);
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = bi + 32 * wr + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+    if (row < M && col < N) {
+      float v;
+      if (KIND == 1) {
+        v = 1.0f - acc[reg];
+      } else {
+        float c2 = (sq[E.off[a] + row] + sq[E.off[b] + col]) - 2.0f * acc[reg];
+        if (c2 < 0.0f) c2 = 0.0f;
+        v = sqrtf(c2);
+      }
+      o[(size_t)row * ld + col] = v;
+    }
+  }
+}
+
+// The nn smallest of every row -> 1, ties lowest column (csm_to_binary); blockIdx.z = matrix.
+__global__ __launch_bounds__(256) void k_ef_binarize(const float* __restrict__ C, int64_t mat_stride, int ld, EfPairs E,
+                                                     double kappa, uint8_t* __restrict__ B, int64_t bmat_stride) {
+  const int p = blockIdx.y, m = blockIdx.z;
+  int a, b, M, N;
+  pair_dims(E, p, &a, &b, &M, &N);
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* x = C + m * mat_stride + (size_t)p * ld * ld + (size_t)row * ld;
+  uint8_t* o = B + m * bmat_stride + (size_t)p * ld * ld + (size_t)row * ld;
+  if (kappa == 0.0) {
+    for (int c = lane; c < N; c += 64) o[c] = 1;
+    return;
+  }
+  const int nn = kappa < 1.0 ? (int)rint(kappa * (double)N) : (int)kappa;  // np.round: half to even
+  if (nn <= 0) {
+    for (int c = lane; c < N; c += 64) o[c] = 0;
+    return;
+  }
+  const int per = (N + 63) / 64;
+  const int c0 = lane * per, c1 = min(N, c0 + per);
+  unsigned lo = 0, hi = 0xffffffffu;
+  while (lo < hi) {
+    const unsigned mid = lo + ((hi - lo) >> 1);
+    int c = 0;
+    for (int k = c0; k < c1; ++k) c += fkey(x[k]) <= mid;
+    if (wave_sum(c) >= nn)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  const unsigned kth = lo;
+  int less = 0, eq = 0;
+  for (int k = c0; k < c1; ++k) {
+    const unsigned kk = fkey(x[k]);
+    less += kk < kth;
+    eq += kk == kth;
+  }
+  const int take_eq = nn - wave_sum(less);
+  int seen = wave_incl_scan(eq) - eq;
+  for (int k = c0; k < c1; ++k) {
+    const unsigned kk = fkey(x[k]);
+    uint8_t v = kk < kth;
+    if (kk == kth) {
+      v = seen < take_eq;
+      ++seen;
+    }
+    o[k] = v;
+  }
+}
+
+// Mean of the k smallest of each row (COLS = false) or column; blockIdx.z = matrix.
+template <bool COLS>
+__global__ __launch_bounds__(256) void k_ef_kmean(const float* __restrict__ C, int64_t mat_stride, int ld, EfPairs E,
+                                                  int k, float* __restrict__ out, int64_t omat_stride) {
+  const int p = blockIdx.y, m = blockIdx.z;
+  int a, b, M, N;
+  pair_dims(E, p, &a, &b, &M, &N);
+  const int line = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int nl = COLS ? N : M, len = COLS ? M : N;
+  if (line >= nl) return;
+  const float* base = C + m * mat_stride + (size_t)p * ld * ld;
+  auto at = [&](int e) { return COLS ? base[(size_t)e * ld + line] : base[(size_t)line * ld + e]; };
+  unsigned lo = 0, hi = 0xffffffffu;
+  while (lo < hi) {
+    const unsigned mid = lo + ((hi - lo) >> 1);
+    int c = 0;
+    for (int e = lane; e < len; e += 64) c += fkey(at(e)) <= mid;
+    if (wave_sum(c) >= k)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  const unsigned kth = lo;
+  float sum = 0.0f, kv = 0.0f;
+  int less = 0;
+  bool has = false;
+  for (int e = lane; e < len; e += 64) {
+    const float v = at(e);
+    const unsigned kk = fkey(v);
+    if (kk < kth) {
+      sum += v;
+      ++less;
+    } else if (kk == kth) {
+      kv = v;
+      has = true;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  kv = __shfl(kv, __builtin_ctzll(__ballot(has)));
+  const int less_all = wave_sum(less);
+  if (lane == 0) out[m * omat_stride + (size_t)p * ld + line] = (sum + (float)(k - less_all) * kv) / (float)k;
+}
+
+// E = exp(-(((0 + W_0) + W_1) + W_2)), W_s = getWCSM(C_s); written over C_0 (elementwise, in place).
+__global__ void k_ef_wsum(float* __restrict__ C, int64_t mat_stride, int ld, EfPairs E, const float* __restrict__ rmean,
+                          const float* __restrict__ cmean, int64_t mean_stride, float mu) {
+  const int p = blockIdx.y;
+  int a, b, M, N;
+  pair_dims(E, p, &a, &b, &M, &N);
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)M * N) return;
+  const int i = (int)(e / N), j = (int)(e - (int64_t)i * N);
+  const size_t idx = (size_t)p * ld * ld + (size_t)i * ld + j;
+  float wsum = 0.0f;
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const float v = C[m * mat_stride + idx];
+    const float eps = ((rmean[m * mean_stride + (size_t)p * ld + i] + cmean[m * mean_stride + (size_t)p * ld + j]) + v) / 3.0f;
+    const float me = mu * eps;
+    wsum = wsum + expf(-(v * v) / (2.0f * (me * me)));
+  }
+  C[idx] = expf(-wsum);
+}
+
+// SW metadata of the 4 matrices of each pair: matrix p*4 + s lives at B[s][p].
+__global__ void k_ef_swmeta(EfPairs E, int P, int ld, int64_t bmat_stride, int64_t* off, int32_t* rows, int32_t* cols,
+                            int32_t* ldm) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  int a, b, M, N;
+  pair_dims(E, p, &a, &b, &M, &N);
+  for (int s = 0; s < 4; ++s) {
+    const int m = p * 4 + s;
+    off[m] = s * bmat_stride + (int64_t)p * ld * ld;
+    rows[m] = M;
+    cols[m] = N;
+    ldm[m] = ld;
+  }
+}
+
+}  // namespace
+}  // namespace acoss
+
+using namespace acoss;
+
+extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const float* chroma, const float* chroma_med,
+                                 const int64_t* block_off, const int32_t* n_blocks, int32_t n_tracks,
+                                 int32_t max_blocks, int32_t d_mfcc, int32_t d_ssm, int32_t d_chroma,
+                                 const int32_t* pairs, int64_t n_pairs, double kappa, int32_t K, float mu,
+                                 double* scores_out, void* hip_stream) {
+  clear_error();
+  if (n_tracks <= 0 || n_pairs < 0 || max_blocks <= 0 || d_mfcc <= 0 || d_ssm <= 0 || d_chroma <= 0 ||
+      d_chroma % 12 != 0 || K <= 0 || K >= max_blocks + 1 || kappa < 0.0 ||
+      (n_pairs > 0 && (!mfcc || !ssm || !chroma || !chroma_med || !block_off || !n_blocks || !pairs || !scores_out))) {
+    set_error("acoss_earlyfusion: bad arguments");
+    return ACOSS_E_ARG;
+  }
+  if (n_pairs == 0) return ACOSS_OK;
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  const int ld = (int)align_up((size_t)max_blocks, 4);
+  // per-track scratch: squared norms of the MFCC and SSM blocks, normalised chroma blocks; the
+  // caller's block_off / n_blocks give the total row count through the last track
+  int64_t h_off = 0;
+  int32_t h_nb = 0;
+  ACOSS_HIP_CHECK(hipMemcpy(&h_off, block_off + (n_tracks - 1), 8, hipMemcpyDeviceToHost));
+  ACOSS_HIP_CHECK(hipMemcpy(&h_nb, n_blocks + (n_tracks - 1), 4, hipMemcpyDeviceToHost));
+  const int64_t nrows = h_off + h_nb;
+  const size_t tr_bytes = align_up((size_t)nrows * 4, 256) * 2 + align_up((size_t)nrows * d_chroma * 4, 256);
+  char* tws = static_cast<char*>(workspace(10, tr_bytes));
+  if (!tws) return ACOSS_E_HIP;
+  float* sq_m = reinterpret_cast<float*>(tws);
+  float* sq_s = reinterpret_cast<float*>(tws + align_up((size_t)nrows * 4, 256));
+  float* chn = reinterpret_cast<float*>(tws + 2 * align_up((size_t)nrows * 4, 256));
+  prof_begin(PH_CSM, s);
+  const unsigned rb = (unsigned)((nrows + 3) / 4);
+  hipLaunchKernelGGL(k_ef_rows, dim3(rb), dim3(256), 0, s, mfcc, nrows, d_mfcc, 0, nullptr, sq_m);
+  ACOSS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_ef_rows, dim3(rb), dim3(256), 0, s, ssm, nrows, d_ssm, 0, nullptr, sq_s);
+  ACOSS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_ef_rows, dim3(rb), dim3(256), 0, s, chroma, nrows, d_chroma, 1, chn, nullptr);
+  ACOSS_LAUNCH_CHECK();
+  prof_end(PH_CSM, s);
+
+  // chunk of pairs: 3 CSMs (E overwrites the first), 4 binary matrices, 6 mean vectors, SW scratch
+  const size_t mat = (size_t)ld * ld;
+  const size_t sw_b = sw_bnd_bytes(ld, ld);
+  const size_t per_pair = 3 * mat * 4 + 4 * mat + 6 * (size_t)ld * 4 + 4 * sw_b + 4 * (8 + 4 + 4 + 4) + 8 + 4;
+  size_t budget = (size_t)4 << 30;
+  if (const char* e = getenv("ACOSS_EF_BYTES")) budget = strtoull(e, nullptr, 10);
+  int64_t chunk = (int64_t)(budget / per_pair);
+  if (chunk < 1) chunk = 1;
+  if (chunk > 65535) chunk = 65535;
+  if (chunk > n_pairs) chunk = n_pairs;
+  char* ws = static_cast<char*>(workspace(11, per_pair * chunk + 16 * 256));
+  if (!ws) return ACOSS_E_HIP;
+  size_t o = 0;
+  auto carve = [&](size_t bytes) {
+    char* r = ws + o;
+    o = align_up(o + bytes, 256);
+    return r;
+  };
+  float* C = reinterpret_cast<float*>(carve(3 * mat * 4 * chunk));
+  uint8_t* Bm = reinterpret_cast<uint8_t*>(carve(4 * mat * chunk));
+  float* rmean = reinterpret_cast<float*>(carve(3 * (size_t)ld * 4 * chunk));
+  float* cmean = reinterpret_cast<float*>(carve(3 * (size_t)ld * 4 * chunk));
+  void* bnd = carve(4 * sw_b * chunk);
+  int64_t* m_off = reinterpret_cast<int64_t*>(carve(4 * 8 * chunk));
+  int32_t* m_rows = reinterpret_cast<int32_t*>(carve(4 * 4 * chunk));
+  int32_t* m_cols = reinterpret_cast<int32_t*>(carve(4 * 4 * chunk));
+  int32_t* m_ld = reinterpret_cast<int32_t*>(carve(4 * 4 * chunk));
+  int* oti = reinterpret_cast<int*>(carve(4 * chunk));
+  int* d_err = reinterpret_cast<int*>(carve(4));
+  const int64_t mstride = (int64_t)mat * chunk;       // between the 3 CSM planes / 4 binary planes
+  const int64_t meanstride = (int64_t)ld * chunk;     // between the 3 mean vectors
+  const int tiles = (ld + kT - 1) / kT;
+  for (int64_t p0 = 0; p0 < n_pairs; p0 += chunk) {
+    const int P = (int)((n_pairs - p0) < chunk ? (n_pairs - p0) : chunk);
+    const EfPairs E{pairs + 2 * p0, block_off, n_blocks};
+    prof_begin(PH_CSM, s);
+    hipLaunchKernelGGL(k_ef_oti, dim3((P + 255) / 256), dim3(256), 0, s, chroma_med, pairs + 2 * p0, P, oti);
+    ACOSS_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ef_csm<0>, dim3(tiles, tiles, P), dim3(256), 0, s, mfcc, d_mfcc, sq_m, E, oti, ld, C);
+    ACOSS_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ef_csm<0>, dim3(tiles, tiles, P), dim3(256), 0, s, ssm, d_ssm, sq_s, E, oti, ld,
+                       C + mstride);
+    ACOSS_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ef_csm<1>, dim3(tiles, tiles, P), dim3(256), 0, s, chn, d_chroma, nullptr, E, oti, ld,
+                       C + 2 * mstride);
+    ACOSS_LAUNCH_CHECK();
+    prof_end(PH_CSM, s);
+    prof_begin(PH_BIN, s);
+    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 3) / 4, P, 3), dim3(256), 0, s, C, mstride, ld, E, kappa, Bm,
+                       mstride);
+    ACOSS_LAUNCH_CHECK();
+    prof_end(PH_BIN, s);
+    prof_begin(PH_WCSM, s);
+    hipLaunchKernelGGL(k_ef_kmean<false>, dim3((ld + 3) / 4, P, 3), dim3(256), 0, s, C, mstride, ld, E, (int)K, rmean,
+                       meanstride);
+    ACOSS_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ef_kmean<true>, dim3((ld + 3) / 4, P, 3), dim3(256), 0, s, C, mstride, ld, E, (int)K, cmean,
+                       meanstride);
+    ACOSS_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ef_wsum, dim3((unsigned)((mat + 255) / 256), P), dim3(256), 0, s, C, mstride, ld, E, rmean,
+                       cmean, meanstride, mu);
+    ACOSS_LAUNCH_CHECK();
+    prof_end(PH_WCSM, s);
+    prof_begin(PH_BIN, s);
+    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 3) / 4, P, 1), dim3(256), 0, s, C, mstride, ld, E, kappa,
+                       Bm + 3 * mstride, mstride);
+    ACOSS_LAUNCH_CHECK();
+    prof_end(PH_BIN, s);
+    prof_begin(PH_SW, s);
+    hipLaunchKernelGGL(k_ef_swmeta, dim3((P + 255) / 256), dim3(256), 0, s, E, P, ld, mstride, m_off, m_rows, m_cols,
+                       m_ld);
+    ACOSS_LAUNCH_CHECK();
+    ACOSS_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
+    int rc = launch_sw_batch(Bm, m_off, m_rows, m_cols, m_ld, 4 * P, ld, ld, bnd, scores_out + 4 * p0, d_err, s);
+    if (rc) return rc;
+    prof_end(PH_SW, s);
+  }
+  return ACOSS_OK;
+}

@@ -252,11 +252,12 @@ struct SwAbove {
 
 __global__ __launch_bounds__(64) void k_sw(const uint8_t* __restrict__ mats, const int64_t* __restrict__ off,
                                            const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
-                                           double4* __restrict__ bnd, int64_t bnd_stride, double* __restrict__ out,
-                                           int* __restrict__ err) {
+                                           const int32_t* __restrict__ ldm, double4* __restrict__ bnd,
+                                           int64_t bnd_stride, double* __restrict__ out, int* __restrict__ err) {
   const int mid = blockIdx.x;
   const int lane = threadIdx.x;
   const int M = rows[mid], N = cols[mid];
+  const int ldb = ldm ? ldm[mid] : N;  // row stride (padded batches) or dense
   const uint8_t* B = mats + off[mid];
   double best = 0.0;
   if (M < 4 || N < 4) {
@@ -286,7 +287,7 @@ __global__ __launch_bounds__(64) void k_sw(const uint8_t* __restrict__ mats, con
         for (int r = 0; r < kSWR; ++r) {
           const int i = row0 + r;
           if (i < M) {
-            const uint8_t v = B[(size_t)i * N + c];
+            const uint8_t v = B[(size_t)i * ldb + c];
             bad |= v > 1;
             w0 |= (unsigned)(v != 0) << r;
           }
@@ -361,6 +362,26 @@ __global__ __launch_bounds__(64) void k_sw(const uint8_t* __restrict__ mats, con
 }
 
 }  // namespace
+
+// Batched constrained Smith-Waterman for other translation units (earlyfusion.hip): one wave
+// per matrix; ldm (nullable) = row strides; bnd: nbands(max_rows) * align(max_cols, 8) double4
+// per matrix; err (device int) is OR-ed with 1 on a non-binary element.
+int launch_sw_batch(const uint8_t* mats, const int64_t* off, const int32_t* rows, const int32_t* cols,
+                    const int32_t* ldm, int n, int max_rows, int max_cols, void* bnd, double* out, int* err,
+                    hipStream_t s) {
+  const int nbands = (max_rows + 64 * kSWR - 1) / (64 * kSWR);
+  const int64_t bstride = (int64_t)nbands * align_up((size_t)max_cols, 8);
+  hipLaunchKernelGGL(k_sw, dim3(n), dim3(64), 0, s, mats, off, rows, cols, ldm, static_cast<double4*>(bnd), bstride,
+                     out, err);
+  ACOSS_LAUNCH_CHECK();
+  return ACOSS_OK;
+}
+
+size_t sw_bnd_bytes(int max_rows, int max_cols) {
+  const int nbands = (max_rows + 64 * kSWR - 1) / (64 * kSWR);
+  return 32 * (size_t)nbands * align_up((size_t)max_cols, 8);
+}
+
 }  // namespace acoss
 
 using namespace acoss;
@@ -488,7 +509,8 @@ extern "C" int acoss_sw_constrained(const uint8_t* mats, const int64_t* off, con
   int* d_err = reinterpret_cast<int*>(ws);
   double4* bnd = reinterpret_cast<double4*>(ws + 256);
   ACOSS_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
-  hipLaunchKernelGGL(k_sw, dim3(n_mats), dim3(64), 0, s, mats, off, rows, cols, bnd, bstride, score_out, d_err);
+  hipLaunchKernelGGL(k_sw, dim3(n_mats), dim3(64), 0, s, mats, off, rows, cols, nullptr, bnd, bstride, score_out,
+                     d_err);
   ACOSS_LAUNCH_CHECK();
   prof_end(PH_SW, s);
   int h_err = 0;

@@ -146,6 +146,17 @@ int acoss_simple_features(const float* feats, const int64_t* track_off, const in
                           int32_t win, int32_t skip, const double* smooth, int32_t smooth_len, double* out,
                           const int64_t* out_off, int64_t out_elems, void* hip_stream);
 
+/* Batched EarlyFusion scores (A15: EarlyFusion.similarity, acoss/algorithms/earlyfusion_traile.py:157-198).
+ * Block features of every track packed row-major: mfcc (sum nb x d_mfcc), ssm (sum nb x d_ssm),
+ * chroma (sum nb x d_chroma, 12-bin blocks) float32, track t's rows at block_off[t], n_blocks[t]
+ * of them; chroma_med (n_tracks x 12) float32. For every pair: CSMs (euclid, euclid, blocked-OTI
+ * cosine), csm_to_binary(kappa), getWCSM(K, K, mu) fusion, and smith_waterman_constrained of the
+ * four binary matrices -> scores_out[4 p + {0: mfccs, 1: ssms, 2: chromas, 3: early}] (float64). */
+int acoss_earlyfusion(const float* mfcc, const float* ssm, const float* chroma, const float* chroma_med,
+                      const int64_t* block_off, const int32_t* n_blocks, int32_t n_tracks, int32_t max_blocks,
+                      int32_t d_mfcc, int32_t d_ssm, int32_t d_chroma, const int32_t* pairs, int64_t n_pairs,
+                      double kappa, int32_t K, float mu, double* scores_out, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

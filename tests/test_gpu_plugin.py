@@ -147,8 +147,14 @@ def test_earlyfusion_composition(tmp_path, monkeypatch):
         Cc = npo.get_csm_blocked_oti(f1["chromas"], f2["chromas"], f1["chroma_med"], f2["chroma_med"],
                                      npo.get_csm_cosine)
         assert np.mean(npo.csm_to_binary(Cc, ef.kappa) != mats[2]) < 0.01
-        for s, key in enumerate(["mfccs", "ssms", "chromas", "early"]):
-            ref = oracle.sw_constrained(mats[s])
-            assert ef.Ds[key][i, j] == np.float32(ref)  # Ds is float32, like the memmap
+        Wref = sum(npo.getWCSM(c, ef.K, ef.K) for c in (C, npo.get_csm(f1["ssms"], f2["ssms"]), Cc))
+        assert np.mean(npo.csm_to_binary(np.exp(-Wref), ef.kappa) != mats[3]) < 0.02
+    # the batched C-ABI path (acoss_earlyfusion) equals the per-pair composition on every pair
+    for i in range(ef.N):
+        for j in range(i + 1, ef.N):
+            mats = [m.cpu().numpy() for m in ef.pair_matrices(i, j)]
+            for s, key in enumerate(["mfccs", "ssms", "chromas", "early"]):
+                ref = oracle.sw_constrained(mats[s])
+                assert ef.Ds[key][i, j] == np.float32(ref), (i, j, key)  # Ds is float32, like the memmap
     ef.do_late_fusion()
     assert np.all(np.isfinite(ef.Ds["late"])) and np.all(np.isfinite(ef.Ds["early+late"]))
