@@ -13,10 +13,12 @@
 //   k_ef_oti      per pair: get_oti(med_a, med_b), first maximum
 //   k_ef_csm<K>   64x64 MFMA f32 tiles x pairs (blockIdx.z); the OTI roll of the query's 12-bin
 //                 blocks is applied in the tile loader
-//   k_ef_binarize wave per (row, pair, matrix): the round(kappa * N) smallest -> 1, ties lowest column
-//   k_ef_kmean    wave per (row|column, pair, matrix): mean of the K smallest
+//   k_ef_binarize wave per (row, pair, matrix): the round(kappa * N) smallest -> 1, ties lowest
+//                 column; 16 rows per block packed into u16 bit words (the SW input)
+//   k_ef_kmin*    thread per (row|column, pair, matrix): mean of the K smallest (K <= 16;
+//                 k_ef_kmean, a wave-per-line select, beyond that)
 //   k_ef_wsum     elementwise: E = exp(-(((0 + W_m) + W_s) + W_c)) in float32
-//   SW            launch_sw_batch (misc.hip) over the 4P binary matrices
+//   SW            launch_swb_batch (misc.hip) over the 4P bit planes
 // Tolerance vs the reference: the GEMMs' summation order (BLAS vs MFMA); every other step is the
 // reference's float32 arithmetic.
 #include <cmath>
@@ -26,15 +28,16 @@
 
 namespace acoss {
 
-int launch_sw_batch(const uint8_t* mats, const int64_t* off, const int32_t* rows, const int32_t* cols,
-                    const int32_t* ldm, int n, int max_rows, int max_cols, void* bnd, double* out, int* err,
-                    hipStream_t s);
+int launch_swb_batch(const uint16_t* W, int64_t wstride, int ldw, const int32_t* rows, const int32_t* cols, int n,
+                     int max_rows, int max_cols, void* bnd, double* out, hipStream_t s);
 size_t sw_bnd_bytes(int max_rows, int max_cols);
 
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kT = 64, kKC = 32;
+constexpr int kBinRegs = 16;  // row keys per lane kept in registers by k_ef_binarize (N <= 1024)
+constexpr int kKmax = 16;     // largest K of the streaming k-smallest means
 
 __device__ __forceinline__ unsigned fkey(float f) {
   const unsigned u = __builtin_bit_cast(unsigned, f);
@@ -148,37 +151,53 @@ __global__ __launch_bounds__(256) void k_ef_csm(const float* __restrict__ bank, 
   }
 }
 
-// The nn smallest of every row -> 1, ties lowest column (csm_to_binary); blockIdx.z = matrix.
-__global__ __launch_bounds__(256) void k_ef_binarize(const float* __restrict__ C, int64_t mat_stride, int ld, EfPairs E,
-                                                     double kappa, uint8_t* __restrict__ B, int64_t bmat_stride) {
-  const int p = blockIdx.y, m = blockIdx.z;
-  int a, b, M, N;
-  pair_dims(E, p, &a, &b, &M, &N);
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= M) return;
-  const float* x = C + m * mat_stride + (size_t)p * ld * ld + (size_t)row * ld;
-  uint8_t* o = B + m * bmat_stride + (size_t)p * ld * ld + (size_t)row * ld;
+// The nn smallest of every row -> 1, ties lowest column (csm_to_binary). A block of 16 waves
+// takes 16 rows (one wave per row) and writes them as one row of u16 bit words (bit r = row
+// 16g + r) in LDS, then to the pair's bit plane for SW. blockIdx.z = CSM plane, written to
+// bit plane z + plane0 of the pair (plane stride = wplane words, 4 planes per pair).
+__device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int N, double kappa, int lane,
+                                                unsigned* bits, unsigned bit) {
   if (kappa == 0.0) {
-    for (int c = lane; c < N; c += 64) o[c] = 1;
+    for (int c = lane; c < N; c += 64) atomicOr(&bits[c], bit);
     return;
   }
   const int nn = kappa < 1.0 ? (int)rint(kappa * (double)N) : (int)kappa;  // np.round: half to even
-  if (nn <= 0) {
-    for (int c = lane; c < N; c += 64) o[c] = 0;
-    return;
-  }
+  if (nn <= 0) return;
   const int per = (N + 63) / 64;
   const int c0 = lane * per, c1 = min(N, c0 + per);
   unsigned lo = 0, hi = 0xffffffffu;
-  while (lo < hi) {
-    const unsigned mid = lo + ((hi - lo) >> 1);
-    int c = 0;
-    for (int k = c0; k < c1; ++k) c += fkey(x[k]) <= mid;
-    if (wave_sum(c) >= nn)
-      hi = mid;
-    else
-      lo = mid + 1;
+  if (per <= kBinRegs) {  // the row's keys in registers: one pass over memory
+    unsigned kr[kBinRegs];
+#pragma unroll
+    for (int q = 0; q < kBinRegs; ++q) kr[q] = (q < per && c0 + q < c1) ? fkey(x[c0 + q]) : 0xffffffffu;
+    unsigned mn = 0xffffffffu, mx = 0u;  // bound the search by the row's range
+#pragma unroll
+    for (int q = 0; q < kBinRegs; ++q) {
+      mn = min(mn, kr[q]);
+      if (q < per && c0 + q < c1) mx = max(mx, kr[q]);
+    }
+    lo = wave_min_u32(mn);
+    hi = wave_max_u32(mx);
+    while (lo < hi) {
+      const unsigned mid = lo + ((hi - lo) >> 1);
+      int c = 0;
+#pragma unroll
+      for (int q = 0; q < kBinRegs; ++q) c += kr[q] <= mid;
+      if (wave_sum(c) >= nn)
+        hi = mid;
+      else
+        lo = mid + 1;
+    }
+  } else {
+    while (lo < hi) {
+      const unsigned mid = lo + ((hi - lo) >> 1);
+      int c = 0;
+      for (int k = c0; k < c1; ++k) c += fkey(x[k]) <= mid;
+      if (wave_sum(c) >= nn)
+        hi = mid;
+      else
+        lo = mid + 1;
+    }
   }
   const unsigned kth = lo;
   int less = 0, eq = 0;
@@ -191,13 +210,32 @@ __global__ __launch_bounds__(256) void k_ef_binarize(const float* __restrict__ C
   int seen = wave_incl_scan(eq) - eq;
   for (int k = c0; k < c1; ++k) {
     const unsigned kk = fkey(x[k]);
-    uint8_t v = kk < kth;
+    bool v = kk < kth;
     if (kk == kth) {
       v = seen < take_eq;
       ++seen;
     }
-    o[k] = v;
+    if (v) atomicOr(&bits[k], bit);
   }
+}
+
+__global__ __launch_bounds__(1024) void k_ef_binarize(const float* __restrict__ C, int64_t mat_stride, int ld,
+                                                      EfPairs E, double kappa, uint16_t* __restrict__ Wb,
+                                                      int64_t wplane, int plane0) {
+  extern __shared__ unsigned bits[];
+  const int p = blockIdx.y, m = blockIdx.z, g = blockIdx.x;
+  int a, b, M, N;
+  pair_dims(E, p, &a, &b, &M, &N);
+  if (16 * g >= M) return;  // whole block: no barrier skipped by part of it
+  for (int c = threadIdx.x; c < N; c += 1024) bits[c] = 0;
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = 16 * g + w;
+  if (row < M)
+    ef_binarize_row(C + m * mat_stride + (size_t)p * ld * ld + (size_t)row * ld, N, kappa, lane, bits, 1u << w);
+  __syncthreads();
+  uint16_t* o = Wb + ((size_t)p * 4 + plane0 + m) * wplane + (size_t)g * ld;
+  for (int c = threadIdx.x; c < N; c += 1024) o[c] = (uint16_t)bits[c];
 }
 
 // Mean of the k smallest of each row (COLS = false) or column; blockIdx.z = matrix.
@@ -244,6 +282,97 @@ __global__ __launch_bounds__(256) void k_ef_kmean(const float* __restrict__ C, i
   if (lane == 0) out[m * omat_stride + (size_t)p * ld + line] = (sum + (float)(k - less_all) * kv) / (float)k;
 }
 
+// Mean of the k smallest of each row / column, one THREAD per line streaming it once: the k
+// smallest so far stay sorted in registers (one compare rejects most elements, a bubble of
+// min/max inserts the rest). Columns: lanes read consecutive columns (coalesced); rows: each
+// lane walks its own row (cache lines reused along the walk). Sum in ascending order (the
+// reference's np.mean over np.partition output has unspecified order: tolerance).
+template <bool COLS, int KMAX>
+__global__ __launch_bounds__(256) void k_ef_kmin(const float* __restrict__ C, int64_t mat_stride, int ld, EfPairs E,
+                                                 int k, float* __restrict__ out, int64_t omat_stride) {
+  const int p = blockIdx.y, m = blockIdx.z;
+  int a, b, M, N;
+  pair_dims(E, p, &a, &b, &M, &N);
+  const int line = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nl = COLS ? N : M, len = COLS ? M : N;
+  if (line >= nl) return;
+  const float* base = C + m * mat_stride + (size_t)p * ld * ld + (COLS ? (size_t)line : (size_t)line * ld);
+  const size_t step = COLS ? (size_t)ld : 1;
+  float top[KMAX];
+#pragma unroll
+  for (int q = 0; q < KMAX; ++q) top[q] = INFINITY;
+  for (int e = 0; e < len; ++e) {
+    float v = base[e * step];
+    float kth = top[0];
+#pragma unroll
+    for (int q = 1; q < KMAX; ++q) kth = (q == k - 1) ? top[q] : kth;
+    if (v < kth) {
+#pragma unroll
+      for (int q = 0; q < KMAX; ++q) {
+        if (q < k) {
+          const float lo = fminf(top[q], v), hi = fmaxf(top[q], v);
+          top[q] = lo;
+          v = hi;
+        }
+      }
+    }
+  }
+  float sum = 0.0f;
+#pragma unroll
+  for (int q = 0; q < KMAX; ++q)
+    if (q < k) sum += top[q];
+  out[m * omat_stride + (size_t)p * ld + line] = sum / (float)k;
+}
+
+// Row variant of k_ef_kmin: a wave takes 64 rows and stages 64 x 64 tiles through LDS with
+// coalesced row-segment loads; lane r then walks row r of the tile (same insertion order as
+// k_ef_kmin<false>: columns ascending).
+template <int KMAX>
+__global__ __launch_bounds__(64) void k_ef_kmin_rows(const float* __restrict__ C, int64_t mat_stride, int ld,
+                                                     EfPairs E, int k, float* __restrict__ out,
+                                                     int64_t omat_stride) {
+  __shared__ float t[64][65];
+  const int p = blockIdx.y, m = blockIdx.z;
+  int a, b, M, N;
+  pair_dims(E, p, &a, &b, &M, &N);
+  const int row0 = blockIdx.x * 64;
+  if (row0 >= M) return;
+  const int lane = threadIdx.x;
+  const float* base = C + m * mat_stride + (size_t)p * ld * ld;
+  const int nr = min(64, M - row0);
+  float top[KMAX];
+#pragma unroll
+  for (int q = 0; q < KMAX; ++q) top[q] = INFINITY;
+  for (int c0 = 0; c0 < N; c0 += 64) {
+    const int nc = min(64, N - c0);
+    __syncthreads();
+    for (int rr = 0; rr < nr; ++rr) t[rr][lane] = lane < nc ? base[(size_t)(row0 + rr) * ld + c0 + lane] : 0.0f;
+    __syncthreads();
+    for (int e = 0; e < nc; ++e) {
+      float v = t[lane][e];
+      float kth = top[0];
+#pragma unroll
+      for (int q = 1; q < KMAX; ++q) kth = (q == k - 1) ? top[q] : kth;
+      if (v < kth) {
+#pragma unroll
+        for (int q = 0; q < KMAX; ++q) {
+          if (q < k) {
+            const float lo = fminf(top[q], v), hi = fmaxf(top[q], v);
+            top[q] = lo;
+            v = hi;
+          }
+        }
+      }
+    }
+  }
+  if (lane >= nr) return;
+  float sum = 0.0f;
+#pragma unroll
+  for (int q = 0; q < KMAX; ++q)
+    if (q < k) sum += top[q];
+  out[m * omat_stride + (size_t)p * ld + row0 + lane] = sum / (float)k;
+}
+
 // E = exp(-(((0 + W_0) + W_1) + W_2)), W_s = getWCSM(C_s); written over C_0 (elementwise, in place).
 __global__ void k_ef_wsum(float* __restrict__ C, int64_t mat_stride, int ld, EfPairs E, const float* __restrict__ rmean,
                           const float* __restrict__ cmean, int64_t mean_stride, float mu) {
@@ -265,19 +394,15 @@ __global__ void k_ef_wsum(float* __restrict__ C, int64_t mat_stride, int ld, EfP
   C[idx] = expf(-wsum);
 }
 
-// SW metadata of the 4 matrices of each pair: matrix p*4 + s lives at B[s][p].
-__global__ void k_ef_swmeta(EfPairs E, int P, int ld, int64_t bmat_stride, int64_t* off, int32_t* rows, int32_t* cols,
-                            int32_t* ldm) {
+// SW metadata of the 4 matrices of each pair (matrix p*4 + s = bit plane s of pair p).
+__global__ void k_ef_swmeta(EfPairs E, int P, int32_t* rows, int32_t* cols) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   int a, b, M, N;
   pair_dims(E, p, &a, &b, &M, &N);
   for (int s = 0; s < 4; ++s) {
-    const int m = p * 4 + s;
-    off[m] = s * bmat_stride + (int64_t)p * ld * ld;
-    rows[m] = M;
-    cols[m] = N;
-    ldm[m] = ld;
+    rows[p * 4 + s] = M;
+    cols[p * 4 + s] = N;
   }
 }
 
@@ -301,6 +426,10 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   if (n_pairs == 0) return ACOSS_OK;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   const int ld = (int)align_up((size_t)max_blocks, 4);
+  if (ld > 16384) {  // k_ef_binarize keeps one u32 per column in LDS
+    set_error("acoss_earlyfusion: more than 16384 blocks in a track");
+    return ACOSS_E_ARG;
+  }
   // per-track scratch: squared norms of the MFCC and SSM blocks, normalised chroma blocks; the
   // caller's block_off / n_blocks give the total row count through the last track
   int64_t h_off = 0;
@@ -327,7 +456,8 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   // chunk of pairs: 3 CSMs (E overwrites the first), 4 binary matrices, 6 mean vectors, SW scratch
   const size_t mat = (size_t)ld * ld;
   const size_t sw_b = sw_bnd_bytes(ld, ld);
-  const size_t per_pair = 3 * mat * 4 + 4 * mat + 6 * (size_t)ld * 4 + 4 * sw_b + 4 * (8 + 4 + 4 + 4) + 8 + 4;
+  const int64_t wplane = (int64_t)((ld + 15) / 16) * ld;  // u16 words of one bit plane
+  const size_t per_pair = 3 * mat * 4 + 4 * (size_t)wplane * 2 + 6 * (size_t)ld * 4 + 4 * sw_b + 4 * (4 + 4) + 4;
   size_t budget = (size_t)4 << 30;
   if (const char* e = getenv("ACOSS_EF_BYTES")) budget = strtoull(e, nullptr, 10);
   int64_t chunk = (int64_t)(budget / per_pair);
@@ -343,17 +473,15 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
     return r;
   };
   float* C = reinterpret_cast<float*>(carve(3 * mat * 4 * chunk));
-  uint8_t* Bm = reinterpret_cast<uint8_t*>(carve(4 * mat * chunk));
+  uint16_t* Wb = reinterpret_cast<uint16_t*>(carve(4 * (size_t)wplane * 2 * chunk));
   float* rmean = reinterpret_cast<float*>(carve(3 * (size_t)ld * 4 * chunk));
   float* cmean = reinterpret_cast<float*>(carve(3 * (size_t)ld * 4 * chunk));
   void* bnd = carve(4 * sw_b * chunk);
-  int64_t* m_off = reinterpret_cast<int64_t*>(carve(4 * 8 * chunk));
   int32_t* m_rows = reinterpret_cast<int32_t*>(carve(4 * 4 * chunk));
   int32_t* m_cols = reinterpret_cast<int32_t*>(carve(4 * 4 * chunk));
-  int32_t* m_ld = reinterpret_cast<int32_t*>(carve(4 * 4 * chunk));
   int* oti = reinterpret_cast<int*>(carve(4 * chunk));
-  int* d_err = reinterpret_cast<int*>(carve(4));
-  const int64_t mstride = (int64_t)mat * chunk;       // between the 3 CSM planes / 4 binary planes
+  const size_t bin_lds = (size_t)ld * 4;
+  const int64_t mstride = (int64_t)mat * chunk;       // between the 3 CSM planes
   const int64_t meanstride = (int64_t)ld * chunk;     // between the 3 mean vectors
   const int tiles = (ld + kT - 1) / kT;
   for (int64_t p0 = 0; p0 < n_pairs; p0 += chunk) {
@@ -372,32 +500,39 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_CSM, s);
     prof_begin(PH_BIN, s);
-    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 3) / 4, P, 3), dim3(256), 0, s, C, mstride, ld, E, kappa, Bm,
-                       mstride);
+    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 3), dim3(1024), bin_lds, s, C, mstride, ld, E, kappa,
+                       Wb, wplane, 0);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_BIN, s);
     prof_begin(PH_WCSM, s);
-    hipLaunchKernelGGL(k_ef_kmean<false>, dim3((ld + 3) / 4, P, 3), dim3(256), 0, s, C, mstride, ld, E, (int)K, rmean,
-                       meanstride);
-    ACOSS_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ef_kmean<true>, dim3((ld + 3) / 4, P, 3), dim3(256), 0, s, C, mstride, ld, E, (int)K, cmean,
-                       meanstride);
-    ACOSS_LAUNCH_CHECK();
+    if (K <= kKmax) {
+      hipLaunchKernelGGL((k_ef_kmin_rows<kKmax>), dim3((ld + 63) / 64, P, 3), dim3(64), 0, s, C, mstride, ld, E,
+                         (int)K, rmean, meanstride);
+      ACOSS_LAUNCH_CHECK();
+      hipLaunchKernelGGL((k_ef_kmin<true, kKmax>), dim3((ld + 255) / 256, P, 3), dim3(256), 0, s, C, mstride, ld, E,
+                         (int)K, cmean, meanstride);
+      ACOSS_LAUNCH_CHECK();
+    } else {
+      hipLaunchKernelGGL(k_ef_kmean<false>, dim3((ld + 3) / 4, P, 3), dim3(256), 0, s, C, mstride, ld, E, (int)K,
+                         rmean, meanstride);
+      ACOSS_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_ef_kmean<true>, dim3((ld + 3) / 4, P, 3), dim3(256), 0, s, C, mstride, ld, E, (int)K,
+                         cmean, meanstride);
+      ACOSS_LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL(k_ef_wsum, dim3((unsigned)((mat + 255) / 256), P), dim3(256), 0, s, C, mstride, ld, E, rmean,
                        cmean, meanstride, mu);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_WCSM, s);
     prof_begin(PH_BIN, s);
-    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 3) / 4, P, 1), dim3(256), 0, s, C, mstride, ld, E, kappa,
-                       Bm + 3 * mstride, mstride);
+    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 1), dim3(1024), bin_lds, s, C, mstride, ld, E, kappa,
+                       Wb, wplane, 3);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_BIN, s);
     prof_begin(PH_SW, s);
-    hipLaunchKernelGGL(k_ef_swmeta, dim3((P + 255) / 256), dim3(256), 0, s, E, P, ld, mstride, m_off, m_rows, m_cols,
-                       m_ld);
+    hipLaunchKernelGGL(k_ef_swmeta, dim3((P + 255) / 256), dim3(256), 0, s, E, P, m_rows, m_cols);
     ACOSS_LAUNCH_CHECK();
-    ACOSS_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
-    int rc = launch_sw_batch(Bm, m_off, m_rows, m_cols, m_ld, 4 * P, ld, ld, bnd, scores_out + 4 * p0, d_err, s);
+    int rc = launch_swb_batch(Wb, wplane, ld, m_rows, m_cols, 4 * P, ld, ld, bnd, scores_out + 4 * p0, s);
     if (rc) return rc;
     prof_end(PH_SW, s);
   }

@@ -236,91 +236,90 @@ __global__ void k_wcsm_apply(const float* __restrict__ C, int M, int N, const fl
 }
 
 // ---------------------------------------------------------------------------------------
-// smith_waterman_constrained in float64, one wave per matrix. Lane l owns 16 rows of a
-// 1024-row band and sweeps the columns skewed by one per lane; boundary rows (2 of S,
-// 3 of B) pass down with __shfl_up; bands chain through global memory.
+// smith_waterman_constrained in float64, one wave per matrix. The binary matrix arrives as a
+// bit plane: word W[g][c] (u16) holds rows 16g..16g+15 of column c. Lane l owns R rows of a
+// 64R-row band and sweeps the columns skewed by one per lane, reading one word per column
+// (prefetched four columns ahead); boundary rows (2 of S, 3 of B) pass down with __shfl_up;
+// bands chain through global memory.
 //   S[i][j] = max((S[i-1][j-1] + m) + d(B[i-2][j-2]), (S[i-2][j-1] + m) + d(B[i-3][j-2]),
 //                 (S[i-1][j-2] + m) + d(B[i-2][j-3]), 0),  i, j >= 3,
 //   m = B[i-1][j-1] ? 1 : -1,  d(v) = v > 0 ? 0 : -0.7   (alignment_tools.py:7-46)
+// R = 8 when the batch's matrices have <= 512 rows (56 of 64 lanes busy at 446 rows), else 16.
 // ---------------------------------------------------------------------------------------
-constexpr int kSWR = 16;
-
 struct SwAbove {
-  double s13, s14, s15;  // S rows 13..15 of the lane above (only 14, 15 used)
-  unsigned b;            // B bits rows 13, 14, 15 (bits 0..2)
+  double sa, sb;  // S rows R-2, R-1 of the lane above
+  unsigned b;     // B bits rows R-3, R-2, R-1 (bits 0..2)
 };
 
-__global__ __launch_bounds__(64) void k_sw(const uint8_t* __restrict__ mats, const int64_t* __restrict__ off,
-                                           const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
-                                           const int32_t* __restrict__ ldm, double4* __restrict__ bnd,
-                                           int64_t bnd_stride, double* __restrict__ out, int* __restrict__ err) {
+template <int R>
+__global__ __launch_bounds__(64) void k_swb(const uint16_t* __restrict__ W, int64_t wstride, int ldw,
+                                            const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                                            double4* __restrict__ bnd, int64_t bnd_stride, double* __restrict__ out) {
+  static_assert(R == 8 || R == 16, "rows per lane");
+  constexpr unsigned kMask = (1u << R) - 1;
   const int mid = blockIdx.x;
   const int lane = threadIdx.x;
   const int M = rows[mid], N = cols[mid];
-  const int ldb = ldm ? ldm[mid] : N;  // row stride (padded batches) or dense
-  const uint8_t* B = mats + off[mid];
-  double best = 0.0;
   if (M < 4 || N < 4) {
     if (lane == 0) out[mid] = 0.0;
     return;
   }
-  const int nbands = (M + 64 * kSWR - 1) / (64 * kSWR);
-  bool bad = false;
+  const uint16_t* Wm = W + (size_t)mid * wstride;
+  const int nbands = (M + 64 * R - 1) / (64 * R);
+  double best = 0.0;
   for (int band = 0; band < nbands; ++band) {
-    const int row0 = band * 64 * kSWR + lane * kSWR;
+    const int row0 = band * 64 * R + lane * R;
+    const bool rows_ok = row0 < M;
+    const uint16_t* wr = Wm + (size_t)(row0 >> 4) * ldw;
+    const int sh = row0 & 15;
+    auto word = [&](int c) -> unsigned {
+      return (rows_ok && c >= 0 && c < N) ? (((unsigned)wr[c] >> sh) & kMask) : 0u;
+    };
     double4* bout = bnd + (size_t)mid * bnd_stride + (size_t)band * N;
     const double4* bin = bnd + (size_t)mid * bnd_stride + (size_t)(band - 1) * N;
-    double s1[kSWR], s2[kSWR];  // columns c-1, c-2
+    const int lanes = min(64, (M - band * 64 * R + R - 1) / R);  // lanes holding rows of this band
+    double s1[R], s2[R];                                         // columns c-1, c-2
 #pragma unroll
-    for (int r = 0; r < kSWR; ++r) s1[r] = s2[r] = 0.0;
+    for (int r = 0; r < R; ++r) s1[r] = s2[r] = 0.0;
     unsigned w1 = 0, w2 = 0, w3 = 0;  // B bits of my rows at c-1, c-2, c-3
-    SwAbove h1{0, 0, 0, 0}, h2{0, 0, 0, 0}, h3{0, 0, 0, 0};  // from above, columns c-1..c-3
-    double p14 = 0.0, p15 = 0.0;
-    unsigned pb = 0;
-    const int S_end = N + 63;
+    SwAbove h1{0, 0, 0}, h2{0, 0, 0}, h3{0, 0, 0};
+    double pa = 0.0, pb = 0.0;
+    unsigned pbits = 0;
+    unsigned q0 = word(-lane), q1 = word(1 - lane), q2 = word(2 - lane), q3 = word(3 - lane);
+    const int S_end = N + lanes - 1;
     for (int s = 0; s < S_end; ++s) {
       const int c = s - lane;
-      // column c of my rows
-      unsigned w0 = 0;
-      if (c >= 0 && c < N) {
-#pragma unroll
-        for (int r = 0; r < kSWR; ++r) {
-          const int i = row0 + r;
-          if (i < M) {
-            const uint8_t v = B[(size_t)i * ldb + c];
-            bad |= v > 1;
-            w0 |= (unsigned)(v != 0) << r;
-          }
-        }
-      }
-      // from the lane above: its column c (computed last step)
+      const unsigned w0 = q0;
+      q0 = q1;
+      q1 = q2;
+      q2 = q3;
+      q3 = word(c + 4);
       SwAbove h0;
-      h0.s14 = __shfl_up(p14, 1);
-      h0.s15 = __shfl_up(p15, 1);
-      h0.b = (unsigned)__shfl_up((int)pb, 1);
-      h0.s13 = 0.0;
+      h0.sa = __shfl_up(pa, 1);
+      h0.sb = __shfl_up(pb, 1);
+      h0.b = (unsigned)__shfl_up((int)pbits, 1);
       if (lane == 0) {
         if (band > 0 && c >= 0 && c < N) {
           const double4 v = bin[c];
-          h0.s14 = v.x;
-          h0.s15 = v.y;
+          h0.sa = v.x;
+          h0.sb = v.y;
           h0.b = (unsigned)v.z;
         } else {
-          h0.s14 = h0.s15 = 0.0;
+          h0.sa = h0.sb = 0.0;
           h0.b = 0;
         }
       }
       // extended bit words: bit r+3 <-> my row r; bits 0..2 <-> rows -3..-1
-      const uint64_t e1 = ((uint64_t)w1 << 3) | h1.b;
-      const uint64_t e2 = ((uint64_t)w2 << 3) | h2.b;
-      const uint64_t e3 = ((uint64_t)w3 << 3) | h3.b;
+      const uint32_t e1 = (w1 << 3) | h1.b;
+      const uint32_t e2 = (w2 << 3) | h2.b;
+      const uint32_t e3 = (w3 << 3) | h3.b;
       const bool cok = c >= 3 && c < N;
-      double s0[kSWR];
+      double s0[R];
 #pragma unroll
-      for (int r = 0; r < kSWR; ++r) {
-        const double A = r >= 1 ? s1[r - 1] : h1.s15;                    // S[i-1][c-1]
-        const double Bv = r >= 2 ? s1[r - 2] : (r == 1 ? h1.s15 : h1.s14);  // S[i-2][c-1]
-        const double Cv = r >= 1 ? s2[r - 1] : h2.s15;                   // S[i-1][c-2]
+      for (int r = 0; r < R; ++r) {
+        const double A = r >= 1 ? s1[r - 1] : h1.sb;                     // S[i-1][c-1]
+        const double Bv = r >= 2 ? s1[r - 2] : (r == 1 ? h1.sb : h1.sa);  // S[i-2][c-1]
+        const double Cv = r >= 1 ? s2[r - 1] : h2.sb;                    // S[i-1][c-2]
         const double mv = ((e1 >> (r + 2)) & 1) ? 1.0 : -1.0;            // B[i-1][c-1]
         const double d1 = ((e2 >> (r + 1)) & 1) ? 0.0 : -0.7;            // B[i-2][c-2]
         const double d2 = ((e2 >> r) & 1) ? 0.0 : -0.7;                  // B[i-3][c-2]
@@ -337,12 +336,12 @@ __global__ __launch_bounds__(64) void k_sw(const uint8_t* __restrict__ mats, con
         best = v > best ? v : best;
         s0[r] = v;
       }
-      p14 = s0[14];
-      p15 = s0[15];
-      pb = (w0 >> 13) & 7u;
-      if (lane == 63 && band + 1 < nbands && c >= 0 && c < N) bout[c] = make_double4(p14, p15, (double)pb, 0.0);
+      pa = s0[R - 2];
+      pb = s0[R - 1];
+      pbits = (w0 >> (R - 3)) & 7u;
+      if (lane == 63 && band + 1 < nbands && c >= 0 && c < N) bout[c] = make_double4(pa, pb, (double)pbits, 0.0);
 #pragma unroll
-      for (int r = 0; r < kSWR; ++r) {
+      for (int r = 0; r < R; ++r) {
         s2[r] = s1[r];
         s1[r] = s0[r];
       }
@@ -357,29 +356,55 @@ __global__ __launch_bounds__(64) void k_sw(const uint8_t* __restrict__ mats, con
     __syncthreads();
   }
   best = wave_max(best);
-  if (__ballot(bad) && lane == 0) atomicOr(err, 1);
   if (lane == 0) out[mid] = best;
 }
 
-}  // namespace
-
-// Batched constrained Smith-Waterman for other translation units (earlyfusion.hip): one wave
-// per matrix; ldm (nullable) = row strides; bnd: nbands(max_rows) * align(max_cols, 8) double4
-// per matrix; err (device int) is OR-ed with 1 on a non-binary element.
-int launch_sw_batch(const uint8_t* mats, const int64_t* off, const int32_t* rows, const int32_t* cols,
-                    const int32_t* ldm, int n, int max_rows, int max_cols, void* bnd, double* out, int* err,
-                    hipStream_t s) {
-  const int nbands = (max_rows + 64 * kSWR - 1) / (64 * kSWR);
-  const int64_t bstride = (int64_t)nbands * align_up((size_t)max_cols, 8);
-  hipLaunchKernelGGL(k_sw, dim3(n), dim3(64), 0, s, mats, off, rows, cols, ldm, static_cast<double4*>(bnd), bstride,
-                     out, err);
-  ACOSS_LAUNCH_CHECK();
-  return ACOSS_OK;
+// Byte matrices (acoss_sw_constrained's layout) -> bit planes; flags elements other than 0/1.
+__global__ void k_sw_pack(const uint8_t* __restrict__ mats, const int64_t* __restrict__ off,
+                          const int32_t* __restrict__ rows, const int32_t* __restrict__ cols, uint16_t* __restrict__ W,
+                          int64_t wstride, int ldw, int* __restrict__ err) {
+  const int mid = blockIdx.x, g = blockIdx.y;
+  const int c = blockIdx.z * blockDim.x + threadIdx.x;
+  const int M = rows[mid], N = cols[mid];
+  if (c >= N || 16 * g >= M) return;
+  const uint8_t* B = mats + off[mid];
+  unsigned w = 0;
+  bool bad = false;
+  for (int r = 0; r < 16; ++r) {
+    const int i = 16 * g + r;
+    if (i < M) {
+      const uint8_t v = B[(size_t)i * N + c];
+      bad |= v > 1;
+      w |= (unsigned)(v != 0) << r;
+    }
+  }
+  W[(size_t)mid * wstride + (size_t)g * ldw + c] = (uint16_t)w;
+  if (bad) atomicOr(err, 1);
 }
 
+int sw_rows_per_lane(int max_rows) { return max_rows <= 512 ? 8 : 16; }
+
+}  // namespace
+
 size_t sw_bnd_bytes(int max_rows, int max_cols) {
-  const int nbands = (max_rows + 64 * kSWR - 1) / (64 * kSWR);
-  return 32 * (size_t)nbands * align_up((size_t)max_cols, 8);
+  const int R = sw_rows_per_lane(max_rows);
+  const int nbands = (max_rows + 64 * R - 1) / (64 * R);
+  return nbands > 1 ? 32 * (size_t)nbands * align_up((size_t)max_cols, 8) : 32;
+}
+
+// Batched constrained Smith-Waterman over bit planes (also used by earlyfusion.hip): matrix
+// mid's words start at W + mid * wstride, row stride ldw words; bnd: sw_bnd_bytes per matrix.
+int launch_swb_batch(const uint16_t* W, int64_t wstride, int ldw, const int32_t* rows, const int32_t* cols, int n,
+                     int max_rows, int max_cols, void* bnd, double* out, hipStream_t s) {
+  const int64_t bstride = (int64_t)(sw_bnd_bytes(max_rows, max_cols) / 32);
+  if (sw_rows_per_lane(max_rows) == 8)
+    hipLaunchKernelGGL(k_swb<8>, dim3(n), dim3(64), 0, s, W, wstride, ldw, rows, cols, static_cast<double4*>(bnd),
+                       bstride, out);
+  else
+    hipLaunchKernelGGL(k_swb<16>, dim3(n), dim3(64), 0, s, W, wstride, ldw, rows, cols, static_cast<double4*>(bnd),
+                       bstride, out);
+  ACOSS_LAUNCH_CHECK();
+  return ACOSS_OK;
 }
 
 }  // namespace acoss
@@ -502,16 +527,23 @@ extern "C" int acoss_sw_constrained(const uint8_t* mats, const int64_t* off, con
   if (n_mats == 0) return ACOSS_OK;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   prof_begin(PH_SW, s);
-  const int nbands = (max_rows + 64 * kSWR - 1) / (64 * kSWR);
-  const int64_t bstride = (int64_t)nbands * align_up((size_t)max_cols, 8);
-  char* ws = static_cast<char*>(workspace(7, 256 + 32 * (size_t)bstride * n_mats));
+  const int G = (max_rows + 15) / 16;
+  const int ldw = (int)align_up((size_t)max_cols, 4);
+  const int64_t wstride = (int64_t)G * ldw;
+  const size_t bb = sw_bnd_bytes(max_rows, max_cols);
+  char* ws = static_cast<char*>(workspace(7, 256 + bb * n_mats + align_up((size_t)wstride * 2 * n_mats, 256)));
   if (!ws) return ACOSS_E_HIP;
   int* d_err = reinterpret_cast<int*>(ws);
-  double4* bnd = reinterpret_cast<double4*>(ws + 256);
+  void* bnd = ws + 256;
+  uint16_t* W = reinterpret_cast<uint16_t*>(ws + 256 + bb * n_mats);
   ACOSS_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
-  hipLaunchKernelGGL(k_sw, dim3(n_mats), dim3(64), 0, s, mats, off, rows, cols, nullptr, bnd, bstride, score_out,
-                     d_err);
-  ACOSS_LAUNCH_CHECK();
+  if (G > 0 && max_cols > 0) {
+    hipLaunchKernelGGL(k_sw_pack, dim3(n_mats, G, (max_cols + 255) / 256), dim3(256), 0, s, mats, off, rows, cols, W,
+                       wstride, ldw, d_err);
+    ACOSS_LAUNCH_CHECK();
+  }
+  int rc = launch_swb_batch(W, wstride, ldw, rows, cols, n_mats, max_rows, max_cols, bnd, score_out, s);
+  if (rc) return rc;
   prof_end(PH_SW, s);
   int h_err = 0;
   ACOSS_HIP_CHECK(hipMemcpyAsync(&h_err, d_err, 4, hipMemcpyDeviceToHost, s));

@@ -149,7 +149,7 @@ def main():
     res["simple_2000"] = simple_path(2000, 24, 1 if q else 2, 4)
     print(json.dumps({"simple_2000": res["simple_2000"]}), flush=True)
     with tempfile.TemporaryDirectory() as tmp:
-        res["earlyfusion"] = earlyfusion_path(8 if q else 24, 20000, 4 if q else 8, tmp)
+        res["earlyfusion"] = earlyfusion_path(8 if q else 80, 20000, 4 if q else 8, tmp)
     print(json.dumps({"earlyfusion": res["earlyfusion"]}), flush=True)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
