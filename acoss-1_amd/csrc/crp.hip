@@ -812,9 +812,9 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   if (nbmax > 65535) nbmax = 65535;
   const int64_t nb_alloc = n_pairs < nbmax ? n_pairs : nbmax;
   int64_t sub = nb_alloc;
-  // split sub-batch scratch per pair: full keys row-major (4 B), prefixes column-major (2 B) and
-  // the row-threshold words RT
-  const size_t sub_pair = 6 * (size_t)kstride + 4 * (size_t)mask_stride;
+  // split sub-batch scratch per pair: 16-bit prefixes row-major and strip-major (2 + 2 B per
+  // cell) and the row-threshold words RT
+  const size_t sub_pair = 4 * (size_t)kstride + 4 * (size_t)mask_stride;
   if (split) {
     size_t kbudget = (size_t)1 << 30;  // ~42 pairs at 2000 frames (x2 buffers): fills 256 CUs per launch
     if (const char* e = getenv("ACOSS_KEY_BYTES")) kbudget = strtoull(e, nullptr, 10);
@@ -849,7 +849,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   void* w_kpl[2] = {nullptr, nullptr};
   uint32_t* w_rt[2] = {nullptr, nullptr};
   for (int b = 0; split && b < nbuf; ++b) {
-    w_kpl[b] = static_cast<void*>(carve(6 * (size_t)kstride * sub));
+    w_kpl[b] = static_cast<void*>(carve(4 * (size_t)kstride * sub));
     w_rt[b] = reinterpret_cast<uint32_t*>(carve(4 * (size_t)mask_stride * sub));
   }
   hipStream_t ss[2] = {s, s};

@@ -6,17 +6,17 @@
 //
 //  k_sweep9      one 256-thread block per (32-row strip, pair): diagonal walk (G in
 //                registers, query frames by scalar loads, rolled reference frames in LDS);
-//                every squared-distance key goes to HBM as the FULL 32-bit key row-major
-//                F[i][j] and as its HIGH 16 bits strip-major Hc[i/32][j][i%32] (64 B per
-//                column and strip, a block's columns contiguous; through a rolling LDS tile).
-//  k_sel_rows9   one 512-thread block per (32-row strip, pair), one wave per CRP row: 32 full
-//                keys per lane in registers, the 16-bit prefixes of the two order statistics
-//                by binary search with ballot counts (v_cmp + s_bcnt1), the tied group ranked
-//                on the exact keys -> percentile -> squared-domain threshold T_row; then the
-//                row's "key <= T_row" bits, transposed in LDS into the 32-bit strip words RT.
-//  k_sel_cols9   one wave per CRP column on the 16-bit prefixes: the same select gives T_col,
-//                the tied group's exact keys come from F (one gather round); lane l then
-//                holds rows 32l..32l+31 of the column, i.e. exactly one 32-bit CRP word:
+//                every squared-distance key leaves as its HIGH 16 bits only, twice: row-major
+//                Hr[i][j] (straight from registers, 64 lanes = 64 consecutive columns) and
+//                strip-major Hc[i/32][j][i%32] (64 B per column and strip, through a rolling
+//                LDS tile). No full-key plane: 4 B per cell.
+//  k_sel_rows9   (fused into the sweep block as k_sweep_rows9) one wave per CRP row on Hr: the
+//                16-bit prefixes of the two order statistics by a hinted SWAR-count search,
+//                the tied prefix group's exact keys RECOMPUTED (cell_key, one batched round,
+//                ~20-30 cells) and ranked -> percentile -> squared-domain threshold T_row; then
+//                the row's "key <= T_row" bits, transposed in LDS into the strip words RT.
+//  k_sel_cols9   one wave per CRP column on Hc: the same select gives T_col; lane l then holds
+//                rows 32l..32l+31 of the column, i.e. exactly one 32-bit CRP word:
 //                (key <= T_col bits) & RT[strip l][j].
 #include <cstdlib>
 #include <cstring>
@@ -72,10 +72,57 @@ __device__ __forceinline__ void load_query(const float* base_ptr, int f, float (
   x[8] = c.x; x[9] = c.y; x[10] = c.z; x[11] = c.w;
 }
 
-// Key planes of one pair: full keys row-major (line = CRP row), high 16 bits column-major.
+// Key planes of one pair: high 16 bits of every key, row-major (line = CRP row) and
+// strip-major (line = CRP column).
 struct KeyPlanes {
-  uint32_t* fr;
+  uint16_t* hr;
   uint16_t* hc;
+};
+
+// Exact key of cell (i, j), recomputed in the sweep's canonical order: 12-term fmaf chain per
+// frame pair (cell_gram), sequential 9-term sum, d2 = (NX_i - 2 dot) + NY_j clamped at +0
+// (cell_finish). Valid cells only (i < M', j < N'): every frame is inside its track.
+__device__ __forceinline__ float cell_gram(const PairView& V, int fq, int fr) {
+  const f32x4* x = reinterpret_cast<const f32x4*>(V.X + (size_t)fq * 12);
+  const f32x4* y = reinterpret_cast<const f32x4*>(V.Yr + (size_t)fr * 12);
+  const f32x4 x0 = x[0], x1 = x[1], x2 = x[2], y0 = y[0], y1 = y[1], y2 = y[2];
+  float g = 0.0f;
+  g = __builtin_fmaf(x0.x, y0.x, g);
+  g = __builtin_fmaf(x0.y, y0.y, g);
+  g = __builtin_fmaf(x0.z, y0.z, g);
+  g = __builtin_fmaf(x0.w, y0.w, g);
+  g = __builtin_fmaf(x1.x, y1.x, g);
+  g = __builtin_fmaf(x1.y, y1.y, g);
+  g = __builtin_fmaf(x1.z, y1.z, g);
+  g = __builtin_fmaf(x1.w, y1.w, g);
+  g = __builtin_fmaf(x2.x, y2.x, g);
+  g = __builtin_fmaf(x2.y, y2.y, g);
+  g = __builtin_fmaf(x2.z, y2.z, g);
+  g = __builtin_fmaf(x2.w, y2.w, g);
+  return g;
+}
+
+__device__ __forceinline__ unsigned cell_finish(const PairView& V, int i, int j, float dot) {
+  const float d2 = (V.NXq[i] - 2.0f * dot) + V.NXr[j];
+  return __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
+}
+
+__device__ __forceinline__ unsigned cell_key(const PairView& V, int i, int j) {
+  float dot = 0.0f;
+#pragma unroll 1
+  for (int u = 0; u < kMS; ++u) dot = dot + cell_gram(V, (i + u) * V.tau, (j + u) * V.tau);
+  return cell_finish(V, i, j, dot);
+}
+
+// The cells of one CRP line: element e of row i is (i, e), of column j is (e, j). Holds the
+// pair's pointers by value (a reference to the kernel's PairView would put it on the stack).
+template <bool ROW>
+struct LineCells {
+  PairView V;
+  int fix;
+  __device__ __forceinline__ int qi(int e) const { return ROW ? fix : e; }
+  __device__ __forceinline__ int rj(int e) const { return ROW ? e : fix; }
+  __device__ __forceinline__ unsigned operator()(int e) const { return cell_key(V, qi(e), rj(e)); }
 };
 
 constexpr int kTP = 34;  // tile pitch in halfwords: 17 words, odd -> lane stride hits distinct banks
@@ -96,7 +143,7 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
     asm volatile("" : "+s"(base));
     return *(const __attribute__((address_space(4))) float*)(FAST ? base + r : V.NXq + min(i0 + r, V.Mp - 1));
   };
-  uint32_t* Fr = K.fr + (size_t)p * kstride + (size_t)i0 * ldr;
+  uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
   uint16_t* Hc = K.hc + (size_t)p * kstride;
   auto query = [&](int kk, float (&x)[12]) {
     if (FAST) {
@@ -130,7 +177,7 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
     float xb[2][12];
     f32x4 yb[2][3];
     query(0, xb[0]);
-    uint32_t* frow = Fr;
+    uint16_t* hrow = Hr;
     {
       const f32x4* yp = reinterpret_cast<const f32x4*>(Ys + t * 12);
       yb[0][0] = yp[0];
@@ -170,13 +217,13 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
         for (int u = 0; u < kMS; ++u) dot = dot + gw[(r + u) % kMS];
         const float d2 = (nqr(r) - 2.0f * dot) + Ns[t + r];
         const unsigned key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
-        // full key row-major straight from registers: the 64 lanes write 64 consecutive columns
+        // row-major prefix straight from registers: the 64 lanes write 64 consecutive columns
         const int col = j0 + t + r;
         // out-of-range columns (< 0 or >= Np) land in the pad column ldr - 1 (never read):
         // branchless, no per-row lane masks to keep live
-        if (FAST || r < rows) frow[min((unsigned)col, (unsigned)(ldr - 1))] = key;
-        frow += ldr;  // next row: one scalar add instead of 32 hoisted row pointers
-        asm volatile("" : "+s"(frow));
+        if (FAST || r < rows) hrow[min((unsigned)col, (unsigned)(ldr - 1))] = (uint16_t)(key >> 16);
+        hrow += ldr;  // next row: one scalar add instead of 32 hoisted row pointers
+        asm volatile("" : "+s"(hrow));
         tileT[(t + r) * kTP + r] = (uint16_t)(key >> 16);
       }
     }
@@ -260,10 +307,12 @@ struct Line {
         pv[4 * q + 3] = w.w;
       }
     } else {
+      int nv = n - base;  // opaque per call: no hoisted per-element predicates in callers' loops
+      asm volatile("" : "+v"(nv));
 #pragma unroll
       for (int h = 0; h < KPL / 2; ++h) {
-        const unsigned a = (base + 2 * h < n) ? (unsigned)src[2 * h] : kNone;
-        const unsigned b = (base + 2 * h + 1 < n) ? (unsigned)src[2 * h + 1] : kNone;
+        const unsigned a = (2 * h < nv) ? (unsigned)src[2 * h] : kNone;
+        const unsigned b = (2 * h + 1 < nv) ? (unsigned)src[2 * h + 1] : kNone;
         pv[h] = a | (b << 16);
       }
     }
@@ -305,34 +354,6 @@ struct Line {
       a = (k > x && k != kNone) ? min(a, k) : a;
     }
     return wave_min_u32(a);
-  }
-};
-
-// A line of FULL keys (CRP row from F): f = exact keys, packed prefixes for the search.
-template <int KPL>
-struct LineFull : Line<KPL> {
-  unsigned f[KPL];
-  __device__ __forceinline__ void load_full(const uint32_t* src, int n) {
-    const int lane = threadIdx.x & 63;
-    const int base = lane * KPL;
-    if (base + KPL <= n) {
-#pragma unroll
-      for (int q = 0; q < KPL / 4; ++q) {
-        const uint4 w = reinterpret_cast<const uint4*>(src + base)[q];
-        f[4 * q + 0] = w.x;
-        f[4 * q + 1] = w.y;
-        f[4 * q + 2] = w.z;
-        f[4 * q + 3] = w.w;
-      }
-    } else {
-      // opaque per-lane count: keeps the 32 tail predicates from being hoisted out of the
-      // caller's row loop into (spilled) SGPR masks
-      int nv = n - base;
-      asm volatile("" : "+v"(nv));
-#pragma unroll
-      for (int q = 0; q < KPL; ++q) f[q] = (q < nv) ? src[base + q] : 0xffffffffu;
-    }
-    this->from_full(f);
   }
 };
 
@@ -387,6 +408,7 @@ __device__ __forceinline__ unsigned prefix_of_rank(const Line<KPL>& L, int rho, 
 struct WaveLds {
   int list[64];
   uint32_t words[64];
+  float gv[64 * kMS];  // Gram terms of a group's cells, [member][frame]
 };
 
 // Exact keys of a prefix group (the line elements whose 16-bit prefix is P), computed in ONE
@@ -401,6 +423,8 @@ struct Group {
 template <int KPL, class KF>
 __device__ Group group_keys(const Line<KPL>& L, unsigned P, int g, const KF& keyf, WaveLds& W) {
   const int lane = threadIdx.x & 63;
+  int ebase = lane * KPL;  // opaque: element indices are not hoisted out of callers' loops
+  asm volatile("" : "+v"(ebase));
   int base = 0;
 #pragma unroll
   for (int q = 0; q < KPL; ++q) {
@@ -408,39 +432,28 @@ __device__ Group group_keys(const Line<KPL>& L, unsigned P, int g, const KF& key
     const unsigned long long bal = __ballot(m);
     if (m)
       W.list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] =
-          lane * KPL + q;
+          ebase + q;
     base += __popcll(bal);
+  }
+  __builtin_amdgcn_wave_barrier();
+  // the 9 g Gram terms, one per lane and round (about 2 rounds for a typical group of 10-15)
+  for (int t = lane; t < kMS * g; t += 64) {
+    const int k = t / kMS, u = t - k * kMS;
+    const int e = W.list[k];
+    W.gv[t] = cell_gram(keyf.V, (keyf.qi(e) + u) * keyf.V.tau, (keyf.rj(e) + u) * keyf.V.tau);
   }
   __builtin_amdgcn_wave_barrier();
   Group G;
   G.P = P;
   G.g = g;
   G.elem = lane < g ? W.list[lane] : 0;
-  __builtin_amdgcn_wave_barrier();
-  G.key = lane < g ? keyf(G.elem) : 0xffffffffu;
-  return G;
-}
-
-// Same group from a line that holds its exact keys in registers (no recompute).
-template <int KPL>
-__device__ Group group_keys_full(const LineFull<KPL>& L, unsigned P, int g, WaveLds& W) {
-  const int lane = threadIdx.x & 63;
-  int base = 0;
+  G.key = 0xffffffffu;
+  if (lane < g) {
+    float dot = 0.0f;
 #pragma unroll
-  for (int q = 0; q < KPL; ++q) {
-    const bool m = L.pfx(q) == P;
-    const unsigned long long bal = __ballot(m);
-    if (m)
-      W.list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] =
-          (int)L.f[q];
-    base += __popcll(bal);
+    for (int u = 0; u < kMS; ++u) dot = dot + W.gv[lane * kMS + u];
+    G.key = cell_finish(keyf.V, keyf.qi(G.elem), keyf.rj(G.elem), dot);
   }
-  __builtin_amdgcn_wave_barrier();
-  Group G;
-  G.P = P;
-  G.g = g;
-  G.elem = 0;
-  G.key = lane < g ? (unsigned)W.list[lane] : 0xffffffffu;
   __builtin_amdgcn_wave_barrier();
   return G;
 }
@@ -459,28 +472,103 @@ __device__ __forceinline__ unsigned group_rank(const Group& G, int rho) {
   return (unsigned)lane_bcast((int)G.key, src);
 }
 
-// Large groups (g > 64, long silences): recompute the group's low halves lane by lane, then
-// binary-search the low 16 bits counting group members only.
-template <int KPL, class KF>
-__device__ unsigned big_group_rank(const Line<KPL>& L, unsigned P, int rho, const KF& keyf) {
-  const int base = (threadIdx.x & 63) * KPL;
-  unsigned lw[KPL];
-#pragma unroll
-  for (int q = 0; q < KPL; ++q) lw[q] = 0x10000u;
-  for (int q = 0; q < KPL; ++q)
-    if (L.pfx(q) == P) lw[q] = keyf(base + q) & 0xffffu;
-  unsigned a = 0, b = 0xffffu;
-  while (a < b) {
-    const unsigned mid = (a + b) >> 1;
-    int c = 0;
-#pragma unroll
-    for (int q = 0; q < KPL; ++q) c += __popcll(__ballot(lw[q] <= mid));
-    if (c > rho)
-      b = mid;
-    else
-      a = mid + 1;
+// Keys of ranks rho and rho + 1 inside a batched group (rho + 1 < g), one counting loop.
+__device__ __forceinline__ void group_rank2(const Group& G, int rho, unsigned* v0, unsigned* v1) {
+  const int lane = threadIdx.x & 63;
+  int cl = 0, ce = 0;
+  for (int k = 0; k < G.g; ++k) {
+    const unsigned o = (unsigned)lane_bcast((int)G.key, k);
+    cl += o < G.key;
+    ce += o == G.key;
   }
-  return (P << 16) | a;
+  const bool act = lane < G.g;
+  const int s0 = __builtin_ctzll(__ballot(act && cl <= rho && rho < cl + ce));
+  const int s1 = __builtin_ctzll(__ballot(act && cl <= rho + 1 && rho + 1 < cl + ce));
+  *v0 = (unsigned)lane_bcast((int)G.key, s0);
+  *v1 = (unsigned)lane_bcast((int)G.key, s1);
+}
+
+// Members of prefix group P in rounds of 64: round r lists members [64r, 64r + 64) (line order)
+// in W.list and runs fn(element) on lane k < (members in the round). Per-lane member masks and
+// one wave scan give each lane its members' positions; no per-element register arrays.
+template <int KPL, class F>
+__device__ void group_rounds(const Line<KPL>& L, unsigned P, int g, WaveLds& W, F fn) {
+  const int lane = threadIdx.x & 63;
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < KPL; ++q) m |= (uint32_t)(L.pfx(q) == P) << q;
+  const int cnt = __builtin_popcount(m);
+  int idx = wave_incl_scan(cnt) - cnt;
+  int ebase = lane * KPL;
+  asm volatile("" : "+v"(ebase));
+  for (int r0 = 0; r0 < g; r0 += 64) {
+    while (m && idx < r0 + 64) {
+      const int q = __builtin_ctz(m);
+      m &= m - 1;
+      W.list[idx - r0] = ebase + q;
+      ++idx;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < min(64, g - r0)) fn(W.list[lane]);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Bin of rank rho in a 256-bin LDS histogram (lane l owns bins 4l..4l+3); rho becomes the rank
+// inside that bin.
+__device__ __forceinline__ unsigned hist_bin_of_rank(const unsigned* hist, int* rho) {
+  const int lane = threadIdx.x & 63;
+  const unsigned c0 = hist[4 * lane], c1 = hist[4 * lane + 1], c2 = hist[4 * lane + 2], c3 = hist[4 * lane + 3];
+  const int tot = (int)(c0 + c1 + c2 + c3);
+  const int ex = wave_incl_scan(tot) - tot;
+  const int r = *rho;
+  int bin = -1, below = ex;
+  if (r >= ex && r < ex + tot) {
+    if (r < below + (int)c0) {
+      bin = 0;
+    } else if (r < below + (int)(c0 + c1)) {
+      bin = 1;
+      below += c0;
+    } else if (r < below + (int)(c0 + c1 + c2)) {
+      bin = 2;
+      below += c0 + c1;
+    } else {
+      bin = 3;
+      below += c0 + c1 + c2;
+    }
+  }
+  const int src = __builtin_ctzll(__ballot(bin >= 0));
+  *rho = r - lane_bcast(below, src);
+  return (unsigned)(4 * src + lane_bcast(bin, src));
+}
+
+// Key of rank rho in a large prefix group (g > 64; long silences): two passes of recomputed
+// member keys into 8-bit LDS histograms of the low half (bits 15..8, then 7..0).
+template <int KPL, class KF>
+__device__ unsigned big_group_rank(const Line<KPL>& L, unsigned P, int rho, int g, const KF& keyf, WaveLds& W) {
+  const int lane = threadIdx.x & 63;
+  unsigned* hist = reinterpret_cast<unsigned*>(W.gv);  // 256 bins
+  unsigned hi8 = 0, lo8 = 0;
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int b = lane; b < 256; b += 64) hist[b] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    group_rounds(L, P, g, W, [&](int e) {
+      const unsigned k = keyf(e);
+      if (pass == 0)
+        atomicAdd(&hist[(k >> 8) & 0xffu], 1u);
+      else if (((k >> 8) & 0xffu) == hi8)
+        atomicAdd(&hist[k & 0xffu], 1u);
+    });
+    __builtin_amdgcn_wave_barrier();
+    const unsigned bin = hist_bin_of_rank(hist, &rho);
+    __builtin_amdgcn_wave_barrier();
+    if (pass == 0)
+      hi8 = bin;
+    else
+      lo8 = bin;
+  }
+  return (P << 16) | (hi8 << 8) | lo8;
 }
 
 template <int KPL, class KF>
@@ -490,7 +578,7 @@ __device__ unsigned rank_in_prefix(const Line<KPL>& L, unsigned P, int rho, int 
     if (cache->g < 0 || cache->P != P) *cache = group_keys(L, P, g, keyf, W);
     return group_rank(*cache, rho);
   }
-  return big_group_rank(L, P, rho, keyf);
+  return big_group_rank(L, P, rho, g, keyf, W);
 }
 
 // Threshold (distance units) and squared-domain threshold of a line of n keys; leaves the
@@ -501,73 +589,25 @@ __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF&
   const float q = (float)(n - 1) * kappa;
   const float lo_f = floorf(q), hi_f = ceilf(q);
   const int lo = (int)lo_f, hi = (int)hi_f;
-  unsigned kmin, kmax;
-  L.min_max(&kmin, &kmax);
+  unsigned kmin = 0, kmax = 0x7f80u;  // every real prefix (finite non-negative float) is <= 0x7f80
+  if (*hint == kNoHint) L.min_max(&kmin, &kmax);
   int le, less;
   const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, *hint, &le, &less);
   *hint = Pl;
-  const unsigned vlo = rank_in_prefix(L, Pl, lo - less, le - less, keyf, W, c_lo);
-  unsigned vhi = vlo;
-  if (hi != lo) {
+  unsigned vlo, vhi;
+  if (hi != lo && hi < le && le - less <= 64) {
+    *c_lo = group_keys(L, Pl, le - less, keyf, W);
+    group_rank2(*c_lo, lo - less, &vlo, &vhi);
+  } else {
+    vlo = rank_in_prefix(L, Pl, lo - less, le - less, keyf, W, c_lo);
+    vhi = vlo;
+  }
+  if (hi != lo && !(hi < le && le - less <= 64)) {
     if (hi < le) {
       vhi = rank_in_prefix(L, Pl, hi - less, le - less, keyf, W, c_lo);
     } else {
       const unsigned Ph = L.min_greater(Pl);
       vhi = rank_in_prefix(L, Ph, 0, L.count_le(Ph) - le, keyf, W, c_hi);
-    }
-  }
-  const float slo = sqrt_rn(__builtin_bit_cast(float, vlo));
-  float th;
-  if (lo_f == hi_f) {
-    th = slo;
-  } else {
-    const float shi = sqrt_rn(__builtin_bit_cast(float, vhi));
-    const float aa = slo * (hi_f - q);
-    const float bb = shi * (q - lo_f);
-    th = aa + bb;
-  }
-  *thr = th;
-  *T = sq_threshold(th);
-}
-
-// Row variant of line_threshold: the line holds its exact keys, groups rank from registers;
-// groups above 64 members binary-search the low halves held in registers.
-template <int KPL>
-__device__ unsigned row_rank(const LineFull<KPL>& L, unsigned P, int rho, int g, WaveLds& W) {
-  if (g <= 64) return group_rank(group_keys_full(L, P, g, W), rho);
-  unsigned a = 0, b = 0xffffu;
-  while (a < b) {
-    const unsigned mid = (a + b) >> 1;
-    int c = 0;
-#pragma unroll
-    for (int q = 0; q < KPL; ++q) c += __popcll(__ballot(L.pfx(q) == P && (L.f[q] & 0xffffu) <= mid));
-    if (c > rho)
-      b = mid;
-    else
-      a = mid + 1;
-  }
-  return (P << 16) | a;
-}
-
-template <int KPL>
-__device__ void row_threshold(const LineFull<KPL>& L, int n, float kappa, WaveLds& W, float* thr, float* T,
-                              unsigned* hint) {
-  const float q = (float)(n - 1) * kappa;
-  const float lo_f = floorf(q), hi_f = ceilf(q);
-  const int lo = (int)lo_f, hi = (int)hi_f;
-  unsigned kmin, kmax;
-  L.min_max(&kmin, &kmax);
-  int le, less;
-  const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, *hint, &le, &less);
-  *hint = Pl;
-  const unsigned vlo = row_rank(L, Pl, lo - less, le - less, W);
-  unsigned vhi = vlo;
-  if (hi != lo) {
-    if (hi < le) {
-      vhi = row_rank(L, Pl, hi - less, le - less, W);
-    } else {
-      const unsigned Ph = L.min_greater(Pl);
-      vhi = row_rank(L, Ph, 0, L.count_le(Ph) - le, W);
     }
   }
   const float slo = sqrt_rn(__builtin_bit_cast(float, vlo));
@@ -616,10 +656,13 @@ __device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, 
     __builtin_amdgcn_wave_barrier();
     return word | W.words[lane];
   }
-  const int base = lane * KPL;
-  for (int q = 0; q < KPL; ++q)
-    if (L.pfx(q) == T16) word |= (uint32_t)(keyf(base + q) <= Tbits) << q;
-  return word;
+  W.words[lane] = 0u;  // large group: member bits in rounds of 64
+  __builtin_amdgcn_wave_barrier();
+  group_rounds(L, T16, g, W, [&](int e) {
+    if (keyf(e) <= Tbits) atomicOr(&W.words[e / KPL], 1u << (e % KPL));
+  });
+  __builtin_amdgcn_wave_barrier();
+  return word | W.words[lane];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -636,7 +679,7 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
                                           int64_t rt_stride, int ld, WaveLds* wl, uint32_t (*rowbits)[64]) {
   constexpr int KPL = 32;
   const int i0 = strip * kSR;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // w: wave-uniform (SGPR)
   WaveLds& W = wl[w];
   constexpr int RPW = kSR / NW;  // consecutive rows per wave: each search starts from its neighbour's
   unsigned hint = kNoHint;
@@ -645,17 +688,20 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
     const int i = i0 + r;
     uint32_t word = 0;
     if (i < V.Mp) {
-      LineFull<KPL> L;
-      L.load_full(K.fr + (size_t)p * kstride + (size_t)i * ldr, V.Np);
+      Line<KPL> L;
+      int64_t rowoff = (int64_t)p * kstride + (int64_t)i * ldr;
+      asm volatile("" : "+s"(rowoff));  // per-row address: nothing per lane hoisted out of the loop
+      L.load_lanes(K.hr + rowoff, KPL, V.Np);
+      const LineCells<true> keyf{V, i};
       float th, T;
-      row_threshold(L, V.Np, kappa, W, &th, &T, &hint);
+      Group c_lo, c_hi;
+      c_lo.g = c_hi.g = -1;
+      line_threshold(L, V.Np, kappa, keyf, W, &c_lo, &c_hi, &th, &T, &hint);
       if (lane == 0) {
         thr[(size_t)p * thr_stride + i] = th;
         Tq[(size_t)p * thr_stride + i] = T;
       }
-      const unsigned Tb = __builtin_bit_cast(unsigned, T);
-#pragma unroll
-      for (int q = 0; q < KPL; ++q) word |= (uint32_t)(L.f[q] <= Tb) << q;  // 0xffffffff never <= T
+      word = le_bits(L, __builtin_bit_cast(unsigned, T), keyf, W, c_lo, c_hi);
     }
     rowbits[r][lane] = word;
   }
@@ -708,6 +754,9 @@ __global__ __launch_bounds__(256, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K,
   else
     sweep_body<false>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
   __syncthreads();  // the strip's F rows are complete (block-scope visibility of the global stores)
+#ifdef ACOSS_ABL_NOROWS  // timing ablation only (wrong results): sweep without the row select
+  return;
+#endif
   rows_body<4>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld,
                reinterpret_cast<WaveLds*>(smem), reinterpret_cast<uint32_t(*)[64]>(smem + 4 * sizeof(WaveLds)));
 }
@@ -722,7 +771,7 @@ __global__ __launch_bounds__(256) void k_sel_cols9(CrpBatch B, KeyPlanes K, int 
                                                    uint32_t* __restrict__ maskT, int64_t mask_stride, int ld) {
   constexpr int KPL = 32;
   __shared__ WaveLds wl[4];
-  // neighbouring columns share the lines of RT and of the F gathers: keep them on one XCD
+  // neighbouring columns share the lines of RT and the recomputed cells' frames: keep them on one XCD
   const int lb = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   const int p = lb / gridDim.x;
   const PairView V = pair_view(B, p);
@@ -732,8 +781,7 @@ __global__ __launch_bounds__(256) void k_sel_cols9(CrpBatch B, KeyPlanes K, int 
   const int lane = threadIdx.x & 63;
   Line<KPL> L;
   L.load_lanes(K.hc + (size_t)p * kstride + (size_t)j * kSR, (size_t)ldc * kSR, V.Mp);
-  const uint32_t* Fcol = K.fr + (size_t)p * kstride + j;
-  auto keyf = [&](int e) { return Fcol[(size_t)e * ldc]; };
+  const LineCells<false> keyf{V, j};
   float th, Tc;
   Group c_lo, c_hi;
   c_lo.g = c_hi.g = -1;
@@ -752,14 +800,15 @@ __global__ __launch_bounds__(256) void k_sel_cols9(CrpBatch B, KeyPlanes K, int 
 }  // namespace
 
 // Three-kernel CRP (m = 9, lines up to 2048 keys). Returns 1 if not applicable.
-// kplanes: nb * kstride uint32 full keys, then nb * kstride uint16 prefixes; RT: nb * mask_stride
+// kplanes: nb * kstride uint16 row-major prefixes, then nb * kstride uint16 strip-major ones;
+// RT: nb * mask_stride
 // words (same layout as maskT).
 int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, int ldk, int64_t kstride,
                      uint32_t* RT, float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride,
                      uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s) {
   if (B.m != kMS || L > 2048) return 1;
   const size_t plane = (size_t)nb * kstride;
-  const KeyPlanes K{static_cast<uint32_t*>(kplanes), reinterpret_cast<uint16_t*>(static_cast<uint32_t*>(kplanes) + plane)};
+  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane};
   const int nstrips = (L + kSR - 1) / kSR;
   static const bool fused = [] {
     const char* e = getenv("ACOSS_FUSE_ROWS");
