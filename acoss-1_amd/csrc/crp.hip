@@ -71,6 +71,22 @@ __global__ void k_track_norms(const float* __restrict__ feats, const int64_t* __
   NX[(size_t)t * ldn + s] = acc;
 }
 
+// X2[t][f] = frames f and f + 1 of track t interleaved bin by bin (24 floats; frame n is 0):
+// the operand pairs of the split sweep's packed-FP32 Gram (crp_split.hip).
+__global__ void k_track_pairs(const float* __restrict__ feats, const int64_t* __restrict__ off,
+                              const int32_t* __restrict__ len, int ldn, float* __restrict__ X2) {
+  const int t = blockIdx.x;
+  const int f = blockIdx.y * blockDim.x + threadIdx.x;
+  const int n = len[t];
+  if (f >= n) return;
+  const float* x = feats + (off[t] + f) * 12;
+  float4* o = reinterpret_cast<float4*>(X2 + ((size_t)t * ldn + f) * 24);
+  const bool nx = f + 1 < n;
+#pragma unroll
+  for (int c = 0; c < 6; ++c)
+    o[c] = make_float4(x[2 * c], nx ? x[12 + 2 * c] : 0.0f, x[2 * c + 1], nx ? x[12 + 2 * c + 1] : 0.0f);
+}
+
 // Per pair: OTI index (essentia optimalTranspositionIndex restated) and stacked dims.
 __global__ void k_pair_oti(const float* __restrict__ prof, const int32_t* __restrict__ len,
                            const int32_t* __restrict__ pairs, int64_t n_pairs, int use_oti, int m, int tau,
@@ -729,15 +745,25 @@ int run_mask(const Stage& st, const CrpBatch& B, int nb, int L, int nstrips, con
   return ACOSS_OK;
 }
 
-// Per-track prep into workspace slot 0: prof (n_tracks x 12) | NX (n_tracks x ldn).
+// Per-track prep into workspace slot 0: prof (n_tracks x 12) | NX (n_tracks x ldn) | and, when
+// X2 is requested, the interleaved frame pairs (n_tracks x ldn x 24).
 int run_prep(const float* feats, const int64_t* off, const int32_t* len, int n_tracks, int max_len, int m, int tau,
-             hipStream_t s, float** prof, float** NX, int* ldn) {
+             hipStream_t s, float** prof, float** NX, int* ldn, float** X2 = nullptr) {
   *ldn = (int)align_up((size_t)max_len, 64);
-  const size_t bytes = ((size_t)n_tracks * 12 + (size_t)n_tracks * (*ldn)) * sizeof(float);
+  const size_t base = align_up((size_t)n_tracks * 12 + (size_t)n_tracks * (*ldn), 64);
+  const size_t bytes = (base + (X2 ? (size_t)n_tracks * (*ldn) * 24 : 0)) * sizeof(float);
   float* ws = static_cast<float*>(workspace(0, bytes));
   if (!ws) return ACOSS_E_HIP;
   *prof = ws;
   *NX = ws + (size_t)n_tracks * 12;
+  if (X2) {
+    *X2 = ws + base;
+    if (max_len > 0) {
+      hipLaunchKernelGGL(k_track_pairs, dim3(n_tracks, (max_len + 255) / 256), dim3(256), 0, s, feats, off, len, *ldn,
+                         *X2);
+      ACOSS_LAUNCH_CHECK();
+    }
+  }
   hipLaunchKernelGGL(k_track_profile, dim3((n_tracks + 3) / 4), dim3(64), 0, s, feats, off, len, n_tracks, *prof);
   ACOSS_LAUNCH_CHECK();
   if (max_len > 0) {
@@ -783,7 +809,8 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   float *prof, *NX;
   int ldn;
   prof_begin(PH_PREP, s);
-  if ((rc = run_prep(feats, track_off, track_len, n_tracks, max_len, m, tau, s, &prof, &NX, &ldn))) return rc;
+  float* X2 = nullptr;
+  if ((rc = run_prep(feats, track_off, track_len, n_tracks, max_len, m, tau, s, &prof, &NX, &ldn, &X2))) return rc;
   prof_end(PH_PREP, s);
 
   // per-pair slot: oti, dims, thr/T rows+cols, maskT, band boundary
@@ -884,7 +911,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
       for (int s0 = 0; s0 < nb; s0 += (int)sub, ++k) {
         const int ns = (nb - s0) < sub ? (nb - s0) : (int)sub;
         const int b = two ? (k & 1) : 0;
-        CrpBatch Bs{feats, track_off, track_len, NX, ldn, pb + 2 * s0, w_oti + s0, w_dims + s0, m, tau,
+        CrpBatch Bs{feats, X2, track_off, track_len, NX, ldn, pb + 2 * s0, w_oti + s0, w_dims + s0, m, tau,
                     w_yrot + (size_t)s0 * yrot_stride, yrot_stride};
         if ((rc = launch_crp_split(Bs, ns, L, params->kappa, w_kpl[b], ldk, kstride, w_rt[b],
                                    w_thr_r + (size_t)s0 * thr_stride, w_T_r + (size_t)s0 * thr_stride,
@@ -898,7 +925,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
         ACOSS_HIP_CHECK(hipStreamWaitEvent(s, e1, 0));
       }
     } else {
-      CrpBatch B{feats, track_off, track_len, NX, ldn, pb, w_oti, w_dims, m, tau, w_yrot, yrot_stride};
+      CrpBatch B{feats, X2, track_off, track_len, NX, ldn, pb, w_oti, w_dims, m, tau, w_yrot, yrot_stride};
       prof_begin(PH_SEL_ROWS, s);
       if ((rc = run_select(false, st, B, nb, L, ld, params->kappa, w_thr_r, w_T_r, thr_stride, s))) return rc;
       prof_end(PH_SEL_ROWS, s);
@@ -983,7 +1010,7 @@ extern "C" int acoss_crp_pair(const float* X, int32_t M, const float* Y, int32_t
   ACOSS_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_rotate_ref, dim3(16, 1), dim3(256), 0, s, f, d_off, d_len, d_pairs, d_oti, yrot, (int64_t)0);
   ACOSS_LAUNCH_CHECK();
-  CrpBatch B{f, d_off, d_len, NX, ldn, d_pairs, d_oti, d_dims, m, tau, yrot, 0};
+  CrpBatch B{f, nullptr, d_off, d_len, NX, ldn, d_pairs, d_oti, d_dims, m, tau, yrot, 0};
   if ((rc = run_select(false, st, B, 1, L, ld, params->kappa, thr_r, T_r, (int64_t)ld, s))) return rc;
   if ((rc = run_select(true, st, B, 1, L, ld, params->kappa, thr_c, T_c, (int64_t)ld, s))) return rc;
   if (dist) {

@@ -7,6 +7,7 @@ namespace acoss {
 // One batch of pairs of the Serra09/Chen path, all device pointers.
 struct CrpBatch {
   const float* feats;    // packed (sum n, 12) chroma
+  const float* feats2;   // per track (ldn frames): frames f, f+1 interleaved (24 floats); split path only
   const int64_t* off;    // track row offsets
   const int32_t* len;    // track frame counts
   const float* NX;       // stacked squared norms, track t at NX[t*ldn]

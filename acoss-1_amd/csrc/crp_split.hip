@@ -31,6 +31,7 @@ constexpr int kMS = 9;
 
 struct PairView {
   const float* X;   // query frames
+  const float* X2;  // query frame pairs (f, f + 1) interleaved bin by bin (24 floats per f)
   const float* Yr;  // OTI-rolled reference frames
   int nq, nr, tau;
   const float* NXq;
@@ -42,6 +43,7 @@ __device__ __forceinline__ PairView pair_view(const CrpBatch& B, int p) {
   PairView v;
   const int ta = B.pairs[2 * p], tb = B.pairs[2 * p + 1];
   v.X = B.feats + B.off[ta] * 12;
+  v.X2 = B.feats2 ? B.feats2 + (size_t)ta * B.ldn * 24 : nullptr;
   v.Yr = B.yrot + (size_t)p * B.yrot_stride;
   v.nq = B.len[ta];
   v.nr = B.len[tb];
@@ -61,6 +63,11 @@ constexpr int kSR = 32;                       // rows per strip
 constexpr int kSW = 256;                      // diagonals per panel
 constexpr int kSYRows = kSW + kSR + kMS - 2;  // 295 reference frames per panel
 constexpr int kSCols = kSW + kSR;             // 288 columns touched
+constexpr int kSYRowsE = (kSYRows + 1) & ~1;  // 296: whole frame pairs (packed FAST path)
+// Pair block pitch in floats: 24 used + 4 pad. A ds_read_b128 serves 16 lanes per pass; lane
+// pitch 28 dwords puts those 16 lanes on distinct 4-bank groups (pitch 24 would be 2-way).
+constexpr int kYP = 28;
+constexpr int kYsFloats = (kSYRowsE / 2) * kYP > kSYRows * 12 ? (kSYRowsE / 2) * kYP : kSYRows * 12;
 
 __device__ __forceinline__ void load_query(const float* base_ptr, int f, float (&x)[12]) {
   const float* base = base_ptr + (size_t)f * 12;
@@ -108,9 +115,9 @@ __device__ __forceinline__ unsigned cell_finish(const PairView& V, int i, int j,
 }
 
 __device__ __forceinline__ unsigned cell_key(const PairView& V, int i, int j) {
-  float dot = 0.0f;
+  float dot = cell_gram(V, i * V.tau, j * V.tau);  // as the sweep: G_0, then + G_1 ... + G_8
 #pragma unroll 1
-  for (int u = 0; u < kMS; ++u) dot = dot + cell_gram(V, (i + u) * V.tau, (j + u) * V.tau);
+  for (int u = 1; u < kMS; ++u) dot = dot + cell_gram(V, (i + u) * V.tau, (j + u) * V.tau);
   return cell_finish(V, i, j, dot);
 }
 
@@ -126,6 +133,131 @@ struct LineCells {
 };
 
 constexpr int kTP = 34;  // tile pitch in halfwords: 17 words, odd -> lane stride hits distinct banks
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// FAST path diagonal walk in packed FP32 (v_pk_fma_f32 / v_pk_add_f32): lane = diagonal td of
+// the panel, steps kk (query frame i0 + kk) taken two at a time, so one packed chain gives
+// (G_kk, G_kk+1) and one packed window sum gives rows (r, r + 1). Every element follows the
+// scalar canonical order exactly (fused products, sequential sums); only the pairing is new.
+// A wave holds diagonals of one parity PAR: its step pairs (kk, kk + 1) start at kk = PAR mod 2,
+// so reference frames td + kk, td + kk + 1 are always one aligned pair of the interleaved LDS
+// panel Yp; odd waves take step 0 and step 39 alone (rows 0 and 31 alone).
+template <int PAR>
+__device__ __forceinline__ void diag_pk(const PairView& V, int i0, int td, int j0, const float* Yp,
+                                        const float* Ns, uint16_t* tileT, uint16_t* Hr, int ldr) {
+  constexpr int kSteps = kSR + kMS - 1;  // 40
+  const float* X2b = V.X2 + (size_t)i0 * 24;
+  const float* Nq0 = V.NXq + i0;
+  auto nqr = [&](int r) {  // row norm: a scalar load at a compile-time offset
+    const float* base = Nq0;
+    asm volatile("" : "+s"(base));
+    return *(const __attribute__((address_space(4))) float*)(base + r);
+  };
+  auto xpair = [&](int kk, f32x2 (&x)[12]) {  // (X_{i0+kk}[b], X_{i0+kk+1}[b]), scalar loads
+    const float* base = X2b;
+    asm volatile("" : "+s"(base));
+    const cfloat4* q = (const cfloat4*)(base + kk * 24);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const f32x4 v = q[c];
+      x[2 * c] = f32x2{v.x, v.y};
+      x[2 * c + 1] = f32x2{v.z, v.w};
+    }
+  };
+  auto yblock = [&](int f, f32x2 (&y)[12]) {  // LDS pair block of panel frames (f, f + 1), f even
+    const f32x4* yp = reinterpret_cast<const f32x4*>(Yp + (f >> 1) * kYP);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const f32x4 v = yp[c];
+      y[2 * c] = f32x2{v.x, v.y};
+      y[2 * c + 1] = f32x2{v.z, v.w};
+    }
+  };
+  float G[kSteps];  // fully unrolled: compile-time indices, only a window of them live
+  auto emit = [&](int r, float dot, uint16_t* hrow) {
+    const float d2 = (nqr(r) - 2.0f * dot) + Ns[td + r];
+    const unsigned key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
+    const int col = j0 + td + r;
+    hrow[min((unsigned)col, (unsigned)(ldr - 1))] = (uint16_t)(key >> 16);  // pad column for out-of-range
+    tileT[(td + r) * kTP + r] = (uint16_t)(key >> 16);
+  };
+  auto emit2 = [&](int r, f32x2 dot, uint16_t* hrow) {  // rows r, r + 1 (cells on this diagonal)
+    const f32x2 nq = f32x2{nqr(r), nqr(r + 1)};
+    const f32x2 ny = *reinterpret_cast<const f32x2*>(Ns + td + r);  // td + r even: 8-byte aligned
+    const f32x2 d2 = pk_fma(f32x2{-2.0f, -2.0f}, dot, nq) + ny;  // nq - 2 dot exactly (2 dot is exact)
+    const unsigned k0 = __builtin_bit_cast(unsigned, d2.x > 0.0f ? d2.x : 0.0f);
+    const unsigned k1 = __builtin_bit_cast(unsigned, d2.y > 0.0f ? d2.y : 0.0f);
+    const int col = j0 + td + r;
+    hrow[min((unsigned)col, (unsigned)(ldr - 1))] = (uint16_t)(k0 >> 16);
+    hrow[ldr + min((unsigned)(col + 1), (unsigned)(ldr - 1))] = (uint16_t)(k1 >> 16);
+    tileT[(td + r) * kTP + r] = (uint16_t)(k0 >> 16);
+    tileT[(td + r + 1) * kTP + r + 1] = (uint16_t)(k1 >> 16);
+  };
+  auto window1 = [&](int r) {
+    float dot = G[r];
+#pragma unroll
+    for (int u = 1; u < kMS; ++u) dot = dot + G[r + u];
+    return dot;
+  };
+  auto window2 = [&](int r) {
+    f32x2 dot = f32x2{G[r], G[r + 1]};
+#pragma unroll
+    for (int u = 1; u < kMS; ++u) dot = dot + f32x2{G[r + u], G[r + u + 1]};
+    return dot;
+  };
+  uint16_t* hrow = Hr;
+  auto next_row = [&](int n) {
+    hrow += n * ldr;  // one scalar add per row instead of 32 hoisted row pointers
+    asm volatile("" : "+s"(hrow));
+  };
+  f32x2 xb[12], yb[12];
+  if (PAR == 1) {  // step 0 alone: frame td (odd) is the high half of pair block td - 1
+    xpair(0, xb);
+    yblock(td - 1, yb);
+    float g = __builtin_fmaf(xb[0].x, yb[0].y, 0.0f);
+#pragma unroll
+    for (int b = 1; b < 12; ++b) g = __builtin_fmaf(xb[b].x, yb[b].y, g);
+    G[0] = g;
+  }
+#pragma unroll
+  for (int kk = PAR; kk + 1 < kSteps; kk += 2) {
+    xpair(kk, xb);
+    yblock(td + kk, yb);
+    f32x2 g = pk_fma(xb[0], yb[0], f32x2{0.0f, 0.0f});
+#pragma unroll
+    for (int b = 1; b < 12; ++b) g = pk_fma(xb[b], yb[b], g);
+    G[kk] = g.x;
+    G[kk + 1] = g.y;
+    // rows completed by this pair: r = kk - 8 and kk - 7
+    const int r = kk - (kMS - 1);
+    if (PAR == 0) {
+      if (r >= 0) {
+        emit2(r, window2(r), hrow);
+        next_row(2);
+      }
+    } else {
+      if (r == -1) {  // row 0 alone (needs G_0 .. G_8)
+        emit(0, window1(0), hrow);
+        next_row(1);
+      } else if (r >= 0) {
+        emit2(r, window2(r), hrow);
+        next_row(2);
+      }
+    }
+  }
+  if (PAR == 1) {  // step 39 alone: frame td + 39 (even) is the low half of its pair block
+    xpair(kSteps - 1, xb);
+    yblock(td + kSteps - 1, yb);
+    float g = __builtin_fmaf(xb[0].x, yb[0].x, 0.0f);
+#pragma unroll
+    for (int b = 1; b < 12; ++b) g = __builtin_fmaf(xb[b].x, yb[b].x, g);
+    G[kSteps - 1] = g;
+    emit(kSR - 1, window1(kSR - 1), hrow);
+  }
+}
 
 // FAST: tau == 1, a full 32-row strip and all 40 query frames inside the track, so the query
 // frames and row norms sit at compile-time offsets from one base (s_load immediates) and no
@@ -160,19 +292,41 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
   };
   for (int j0 = -(kSR - 1); j0 < V.Np; j0 += kSW) {
     __syncthreads();
-    for (int e = t; e < kSYRows * 3; e += kSW) {
-      const int b = e / 3, piece = e - b * 3;
-      const int jr = j0 + b;
-      const int f = jr * V.tau;
-      f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (jr >= 0 && f < V.nr) v = reinterpret_cast<const f32x4*>(V.Yr + (size_t)f * 12)[piece];
-      reinterpret_cast<f32x4*>(Ys)[e] = v;
+    if (FAST) {  // pair blocks for diag_pk: Ys[f/2][bin][f&1] (tau == 1)
+      for (int e = t; e < kSYRowsE * 3; e += kSW) {
+        const int f = e / 3, piece = e - f * 3;
+        const int jr = j0 + f;
+        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (jr >= 0 && jr < V.nr) v = reinterpret_cast<const f32x4*>(V.Yr + (size_t)jr * 12)[piece];
+        float* d = Ys + (f >> 1) * kYP + 8 * piece + (f & 1);
+        d[0] = v.x;
+        d[2] = v.y;
+        d[4] = v.z;
+        d[6] = v.w;
+      }
+    } else {
+      for (int e = t; e < kSYRows * 3; e += kSW) {
+        const int b = e / 3, piece = e - b * 3;
+        const int jr = j0 + b;
+        const int f = jr * V.tau;
+        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (jr >= 0 && f < V.nr) v = reinterpret_cast<const f32x4*>(V.Yr + (size_t)f * 12)[piece];
+        reinterpret_cast<f32x4*>(Ys)[e] = v;
+      }
     }
     for (int b = t; b < kSCols; b += kSW) {
       const int jr = j0 + b;
       Ns[b] = (jr >= 0 && jr < V.Np) ? V.NXr[jr] : 0.0f;
     }
     __syncthreads();
+    if (FAST) {
+      const int w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+      const int td = 128 * (w >> 1) + 2 * lane + (w & 1);  // waves of one diagonal parity
+      if (w & 1)
+        diag_pk<1>(V, i0, td, j0, Ys, Ns, tileT, Hr, ldr);
+      else
+        diag_pk<0>(V, i0, td, j0, Ys, Ns, tileT, Hr, ldr);
+    } else {
     float gw[kMS];
     float xb[2][12];
     f32x4 yb[2][3];
@@ -212,9 +366,11 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
       gw[kk % kMS] = g;
       if (kk >= kMS - 1) {
         const int r = kk - (kMS - 1);
-        float dot = 0.0f;
+        // sequential 9-term sum; starting at G_0 instead of 0 + G_0 changes at most the sign of
+        // a zero dot, which (NX - 2 dot) + NY never sees: the keys are bit-identical
+        float dot = gw[r % kMS];
 #pragma unroll
-        for (int u = 0; u < kMS; ++u) dot = dot + gw[(r + u) % kMS];
+        for (int u = 1; u < kMS; ++u) dot = dot + gw[(r + u) % kMS];
         const float d2 = (nqr(r) - 2.0f * dot) + Ns[t + r];
         const unsigned key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
         // row-major prefix straight from registers: the 64 lanes write 64 consecutive columns
@@ -227,6 +383,7 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
         tileT[(t + r) * kTP + r] = (uint16_t)(key >> 16);
       }
     }
+    }  // !FAST
     __syncthreads();
     // columns [j0, j0 + 256) complete: column-major prefixes, 32 rows = 64 B per column
     const int jj = j0 + t;
@@ -253,7 +410,7 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
 }
 
 __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride) {
-  __shared__ __attribute__((aligned(16))) float Ys[kSYRows * 12];
+  __shared__ __attribute__((aligned(16))) float Ys[kYsFloats];
   __shared__ float Ns[kSCols];
   __shared__ __attribute__((aligned(16))) uint16_t tileT[kSCols * kTP];  // [column][row] 16-bit prefixes
   const int p = blockIdx.y;
@@ -449,9 +606,9 @@ __device__ Group group_keys(const Line<KPL>& L, unsigned P, int g, const KF& key
   G.elem = lane < g ? W.list[lane] : 0;
   G.key = 0xffffffffu;
   if (lane < g) {
-    float dot = 0.0f;
+    float dot = W.gv[lane * kMS];
 #pragma unroll
-    for (int u = 0; u < kMS; ++u) dot = dot + W.gv[lane * kMS + u];
+    for (int u = 1; u < kMS; ++u) dot = dot + W.gv[lane * kMS + u];
     G.key = cell_finish(keyf.V, keyf.qi(G.elem), keyf.rj(G.elem), dot);
   }
   __builtin_amdgcn_wave_barrier();
@@ -595,6 +752,11 @@ __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF&
   const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, *hint, &le, &less);
   *hint = Pl;
   unsigned vlo, vhi;
+#ifdef ACOSS_ABL_NOGROUP
+  if (true) {
+    vlo = vhi = Pl << 16;
+  } else
+#endif
   if (hi != lo && hi < le && le - less <= 64) {
     *c_lo = group_keys(L, Pl, le - less, keyf, W);
     group_rank2(*c_lo, lo - less, &vlo, &vhi);
@@ -671,6 +833,29 @@ __device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, 
 // ---------------------------------------------------------------------------------------
 constexpr int kRowWaves = 8;
 
+// In-register transpose of a 32 x 32 bit matrix: a[r] bit q -> a[q] bit r (stage J swaps the
+// off-diagonal J x J sub-blocks).
+template <int J>
+__device__ __forceinline__ void transpose_stage(uint32_t (&a)[32]) {
+  constexpr uint32_t m = J == 16 ? 0x0000ffffu : J == 8 ? 0x00ff00ffu : J == 4 ? 0x0f0f0f0fu : J == 2 ? 0x33333333u
+                                                                                                      : 0x55555555u;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    if (k & J) continue;
+    const uint32_t t = ((a[k] >> J) ^ a[k + J]) & m;
+    a[k + J] ^= t;
+    a[k] ^= t << J;
+  }
+}
+
+__device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {
+  transpose_stage<16>(a);
+  transpose_stage<8>(a);
+  transpose_stage<4>(a);
+  transpose_stage<2>(a);
+  transpose_stage<1>(a);
+}
+
 // Row select of one (32-row strip, pair) by NW waves: wave w takes rows w, w+NW, ...
 template <int NW>
 __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr,
@@ -701,19 +886,34 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
         thr[(size_t)p * thr_stride + i] = th;
         Tq[(size_t)p * thr_stride + i] = T;
       }
+#ifndef ACOSS_ABL_NOLEBITS
       word = le_bits(L, __builtin_bit_cast(unsigned, T), keyf, W, c_lo, c_hi);
+#endif
     }
     rowbits[r][lane] = word;
   }
   __syncthreads();
-  // transpose: word of column j = bit (j & 31) of rowbits[r][j >> 5], r = 0..31
+  // transpose: word of column j = bit (j & 31) of rowbits[r][j >> 5], r = 0..31. Thread b takes
+  // the 32 x 32 bit block of columns 32b..32b+31 and transposes it in registers (five
+  // masked-swap stages, about half an op per bit).
   uint32_t* out = RT + (size_t)p * rt_stride + (size_t)strip * ld;
-  for (int j = threadIdx.x; j < V.Np; j += NW * 64) {
-    const int l = j >> 5, q = j & 31;
-    uint32_t word = 0;
+#ifdef ACOSS_ABL_NOTRANSPOSE
+  return;
+#endif
+  for (int b = threadIdx.x; 32 * b < V.Np; b += NW * 64) {
+    uint32_t a[32];
 #pragma unroll
-    for (int r = 0; r < kSR; ++r) word |= ((rowbits[r][l] >> q) & 1u) << r;
-    out[j] = word;
+    for (int r = 0; r < 32; ++r) a[r] = rowbits[r][b];
+    transpose32(a);
+    uint32_t* o = out + 32 * b;
+    if (32 * b + 32 <= ld) {  // whole block inside the row pitch (ld is a multiple of 32 when Np > 32b)
+#pragma unroll
+      for (int q = 0; q < 32; q += 4) *reinterpret_cast<uint4*>(o + q) = make_uint4(a[q], a[q + 1], a[q + 2], a[q + 3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 32; ++q)
+        if (32 * b + q < V.Np) o[q] = a[q];
+    }
   }
 }
 
@@ -733,7 +933,7 @@ __global__ __launch_bounds__(512, 4) void k_sel_rows9(CrpBatch B, KeyPlanes K, i
 // Sweep and row select fused: the block selects the 32 rows it has just swept, reading its
 // full keys back while they are cache-resident (no second pass over F from HBM, one launch
 // fewer). LDS of the two phases is one union.
-constexpr int kSweepLds = (kSYRows * 12 + kSCols) * 4 + kSCols * kTP * 2;
+constexpr int kSweepLds = (kYsFloats + kSCols) * 4 + kSCols * kTP * 2;
 constexpr int kRowsLds = 4 * (int)sizeof(WaveLds) + kSR * 64 * 4;
 constexpr int kFusedLds = kSweepLds > kRowsLds ? kSweepLds : kRowsLds;
 
@@ -743,7 +943,7 @@ __global__ __launch_bounds__(256, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K,
                                                      int ld) {
   __shared__ __attribute__((aligned(16))) char smem[kFusedLds];
   float* Ys = reinterpret_cast<float*>(smem);
-  float* Ns = Ys + kSYRows * 12;
+  float* Ns = Ys + kYsFloats;
   uint16_t* tileT = reinterpret_cast<uint16_t*>(Ns + kSCols);
   const int p = blockIdx.y;
   const PairView V = pair_view(B, p);
@@ -792,7 +992,11 @@ __global__ __launch_bounds__(256) void k_sel_cols9(CrpBatch B, KeyPlanes K, int 
     Tq[(size_t)p * thr_stride + j] = Tc;
   }
   const size_t w = (size_t)p * mask_stride + (size_t)lane * ld + j;
+#ifdef ACOSS_ABL_NOLEBITS
+  const uint32_t bits = 0;
+#else
   const uint32_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
+#endif
   if (lane * KPL >= V.Mp) return;
   maskT[w] = bits & RT[w];
 }
