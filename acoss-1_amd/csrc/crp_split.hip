@@ -135,6 +135,16 @@ struct LineCells {
 constexpr int kTP = 34;  // tile pitch in halfwords: 17 words, odd -> lane stride hits distinct banks
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// Global-address-space u16 pointer: a pointer pinned to SGPRs by an empty asm loses its address
+// space, and generic (flat) stores count in lgkmcnt too, so every s_waitcnt for the LDS reads
+// would also wait for the previous rows' stores to be acknowledged.
+typedef __attribute__((address_space(1))) uint16_t gu16;
+// Store at a 32-bit byte offset from an SGPR base: global_store_short v_off, v, s[base] (saddr
+// form; a u16 element index would need a 64-bit address per store).
+__device__ __forceinline__ void st_u16(gu16* base, unsigned idx, unsigned v) {
+  typedef __attribute__((address_space(1))) char gchar;
+  *(gu16*)((gchar*)base + idx * 2u) = (uint16_t)v;
+}
 
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
@@ -177,22 +187,22 @@ __device__ __forceinline__ void diag_pk(const PairView& V, int i0, int td, int j
     }
   };
   float G[kSteps];  // fully unrolled: compile-time indices, only a window of them live
-  auto emit = [&](int r, float dot, uint16_t* hrow) {
+  auto emit = [&](int r, float dot, gu16* hrow) {
     const float d2 = (nqr(r) - 2.0f * dot) + Ns[td + r];
     const unsigned key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
     const int col = j0 + td + r;
-    hrow[min((unsigned)col, (unsigned)(ldr - 1))] = (uint16_t)(key >> 16);  // pad column for out-of-range
+    st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), key >> 16);  // pad column for out-of-range
     tileT[(td + r) * kTP + r] = (uint16_t)(key >> 16);
   };
-  auto emit2 = [&](int r, f32x2 dot, uint16_t* hrow) {  // rows r, r + 1 (cells on this diagonal)
+  auto emit2 = [&](int r, f32x2 dot, gu16* hrow) {  // rows r, r + 1 (cells on this diagonal)
     const f32x2 nq = f32x2{nqr(r), nqr(r + 1)};
     const f32x2 ny = *reinterpret_cast<const f32x2*>(Ns + td + r);  // td + r even: 8-byte aligned
     const f32x2 d2 = pk_fma(f32x2{-2.0f, -2.0f}, dot, nq) + ny;  // nq - 2 dot exactly (2 dot is exact)
     const unsigned k0 = __builtin_bit_cast(unsigned, d2.x > 0.0f ? d2.x : 0.0f);
     const unsigned k1 = __builtin_bit_cast(unsigned, d2.y > 0.0f ? d2.y : 0.0f);
     const int col = j0 + td + r;
-    hrow[min((unsigned)col, (unsigned)(ldr - 1))] = (uint16_t)(k0 >> 16);
-    hrow[ldr + min((unsigned)(col + 1), (unsigned)(ldr - 1))] = (uint16_t)(k1 >> 16);
+    st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), k0 >> 16);
+    st_u16(hrow, ldr + min((unsigned)(col + 1), (unsigned)(ldr - 1)), k1 >> 16);
     tileT[(td + r) * kTP + r] = (uint16_t)(k0 >> 16);
     tileT[(td + r + 1) * kTP + r + 1] = (uint16_t)(k1 >> 16);
   };
@@ -208,7 +218,7 @@ __device__ __forceinline__ void diag_pk(const PairView& V, int i0, int td, int j
     for (int u = 1; u < kMS; ++u) dot = dot + f32x2{G[r + u], G[r + u + 1]};
     return dot;
   };
-  uint16_t* hrow = Hr;
+  gu16* hrow = (gu16*)Hr;
   auto next_row = [&](int n) {
     hrow += n * ldr;  // one scalar add per row instead of 32 hoisted row pointers
     asm volatile("" : "+s"(hrow));
@@ -290,20 +300,46 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
       load_query(V.X, min((i0 + kk) * V.tau, V.nq - 1), x);
     }
   };
+  // FAST: the next panel's reference frames and norms are fetched into registers while this
+  // panel is swept, and written to LDS after the next barrier (no exposed HBM latency per panel)
+  constexpr int kPF = (kSYRowsE * 3 + kSW - 1) / kSW;  // float4 pieces per thread (4)
+  constexpr int kPN = (kSCols + kSW - 1) / kSW;        // norms per thread (2)
+  f32x4 pf[kPF];
+  float pn[kPN];
+  auto fetch = [&](int j0) {
+#pragma unroll
+    for (int k = 0; k < kPF; ++k) {
+      const int e = t + k * kSW;
+      const int f = e / 3, piece = e - f * 3;
+      const int jr = j0 + f;
+      pf[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (e < kSYRowsE * 3 && jr >= 0 && jr < V.nr) pf[k] = reinterpret_cast<const f32x4*>(V.Yr + (size_t)jr * 12)[piece];
+    }
+#pragma unroll
+    for (int k = 0; k < kPN; ++k) {
+      const int b = t + k * kSW, jr = j0 + b;
+      pn[k] = (b < kSCols && jr >= 0 && jr < V.Np) ? V.NXr[jr] : 0.0f;
+    }
+  };
+  if (FAST) fetch(-(kSR - 1));
   for (int j0 = -(kSR - 1); j0 < V.Np; j0 += kSW) {
     __syncthreads();
     if (FAST) {  // pair blocks for diag_pk: Ys[f/2][bin][f&1] (tau == 1)
-      for (int e = t; e < kSYRowsE * 3; e += kSW) {
-        const int f = e / 3, piece = e - f * 3;
-        const int jr = j0 + f;
-        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (jr >= 0 && jr < V.nr) v = reinterpret_cast<const f32x4*>(V.Yr + (size_t)jr * 12)[piece];
-        float* d = Ys + (f >> 1) * kYP + 8 * piece + (f & 1);
-        d[0] = v.x;
-        d[2] = v.y;
-        d[4] = v.z;
-        d[6] = v.w;
+#pragma unroll
+      for (int k = 0; k < kPF; ++k) {
+        const int e = t + k * kSW;
+        if (e < kSYRowsE * 3) {
+          const int f = e / 3, piece = e - f * 3;
+          float* d = Ys + (f >> 1) * kYP + 8 * piece + (f & 1);
+          d[0] = pf[k].x;
+          d[2] = pf[k].y;
+          d[4] = pf[k].z;
+          d[6] = pf[k].w;
+        }
       }
+#pragma unroll
+      for (int k = 0; k < kPN; ++k)
+        if (t + k * kSW < kSCols) Ns[t + k * kSW] = pn[k];
     } else {
       for (int e = t; e < kSYRows * 3; e += kSW) {
         const int b = e / 3, piece = e - b * 3;
@@ -314,12 +350,15 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
         reinterpret_cast<f32x4*>(Ys)[e] = v;
       }
     }
-    for (int b = t; b < kSCols; b += kSW) {
-      const int jr = j0 + b;
-      Ns[b] = (jr >= 0 && jr < V.Np) ? V.NXr[jr] : 0.0f;
+    if (!FAST) {
+      for (int b = t; b < kSCols; b += kSW) {
+        const int jr = j0 + b;
+        Ns[b] = (jr >= 0 && jr < V.Np) ? V.NXr[jr] : 0.0f;
+      }
     }
     __syncthreads();
     if (FAST) {
+      if (j0 + kSW < V.Np) fetch(j0 + kSW);
       const int w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
       const int td = 128 * (w >> 1) + 2 * lane + (w & 1);  // waves of one diagonal parity
       if (w & 1)
@@ -331,7 +370,7 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
     float xb[2][12];
     f32x4 yb[2][3];
     query(0, xb[0]);
-    uint16_t* hrow = Hr;
+    gu16* hrow = (gu16*)Hr;
     {
       const f32x4* yp = reinterpret_cast<const f32x4*>(Ys + t * 12);
       yb[0][0] = yp[0];
@@ -377,7 +416,7 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
         const int col = j0 + t + r;
         // out-of-range columns (< 0 or >= Np) land in the pad column ldr - 1 (never read):
         // branchless, no per-row lane masks to keep live
-        if (FAST || r < rows) hrow[min((unsigned)col, (unsigned)(ldr - 1))] = (uint16_t)(key >> 16);
+        if (FAST || r < rows) st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), key >> 16);
         hrow += ldr;  // next row: one scalar add instead of 32 hoisted row pointers
         asm volatile("" : "+s"(hrow));
         tileT[(t + r) * kTP + r] = (uint16_t)(key >> 16);
@@ -483,10 +522,17 @@ struct Line {
   // borrow across fields; popcount on VALU, one DPP wave sum (no SGPR per compare, no SALU).
   __device__ __forceinline__ int count_le(unsigned x) const {
     const unsigned X2 = (x + 0x8000u) * 0x10001u;
+#ifdef ACOSS_CNT_ILP
+    unsigned c[4] = {0, 0, 0, 0};  // four independent v_bcnt chains
+#pragma unroll
+    for (int h = 0; h < KPL / 2; ++h) c[h & 3] = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c[h & 3];
+    return wave_sum((int)((c[0] + c[1]) + (c[2] + c[3])));
+#else
     unsigned c = 0;
 #pragma unroll
     for (int h = 0; h < KPL / 2; ++h) c = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c;
     return wave_sum((int)c);
+#endif
   }
   // min over elements (kNone is above every real prefix) and max over real elements
   // (kNone + 1 wraps to 0x8000, masked to 0: below every real prefix + 1)
@@ -868,15 +914,21 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
   WaveLds& W = wl[w];
   constexpr int RPW = kSR / NW;  // consecutive rows per wave: each search starts from its neighbour's
   unsigned hint = kNoHint;
+  // the next row's line is loaded while this one is searched (its latency hidden)
+  auto load_row = [&](Line<KPL>& Ld, int i) {
+    int64_t rowoff = (int64_t)p * kstride + (int64_t)i * ldr;
+    asm volatile("" : "+s"(rowoff));  // per-row address: nothing per lane hoisted out of the loop
+    Ld.load_lanes(K.hr + rowoff, KPL, V.Np);
+  };
+  Line<KPL> Lnext;
+  if (i0 + w * RPW < V.Mp) load_row(Lnext, i0 + w * RPW);
 #pragma unroll 1
   for (int r = w * RPW; r < (w + 1) * RPW; ++r) {
     const int i = i0 + r;
     uint32_t word = 0;
     if (i < V.Mp) {
-      Line<KPL> L;
-      int64_t rowoff = (int64_t)p * kstride + (int64_t)i * ldr;
-      asm volatile("" : "+s"(rowoff));  // per-row address: nothing per lane hoisted out of the loop
-      L.load_lanes(K.hr + rowoff, KPL, V.Np);
+      const Line<KPL> L = Lnext;
+      if (r + 1 < (w + 1) * RPW && i + 1 < V.Mp) load_row(Lnext, i + 1);
       const LineCells<true> keyf{V, i};
       float th, T;
       Group c_lo, c_hi;
@@ -962,10 +1014,21 @@ __global__ __launch_bounds__(256, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K,
 }
 
 // ---------------------------------------------------------------------------------------
-// k_sel_cols9: one wave per CRP column; emits T_col and the column's CRP words.
-// Lane l <-> rows 32l..32l+31 (KPL == 32).
+// k_sel_cols9: one wave per run of kCPW consecutive CRP columns; emits T_col and the columns'
+// CRP words. Lane l <-> rows 32l..32l+31 (KPL == 32). Neighbouring columns share 8 of their 9
+// stacked frames, so each column's search starts from the previous column's answer (the first
+// column of a run bisects from its min/max).
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
+#ifndef ACOSS_CPW
+#define ACOSS_CPW 4
+#endif
+constexpr int kCPW = ACOSS_CPW;
+#ifndef ACOSS_COLS_WPE
+#define ACOSS_COLS_WPE 4
+#endif
+constexpr int kColsPerBlock = 4 * kCPW;
+
+__global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
                                                    const uint32_t* __restrict__ RT, float* __restrict__ thr,
                                                    float* __restrict__ Tq, int64_t thr_stride,
                                                    uint32_t* __restrict__ maskT, int64_t mask_stride, int ld) {
@@ -975,30 +1038,40 @@ __global__ __launch_bounds__(256) void k_sel_cols9(CrpBatch B, KeyPlanes K, int 
   const int lb = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   const int p = lb / gridDim.x;
   const PairView V = pair_view(B, p);
-  const int j = (lb - p * gridDim.x) * 4 + (threadIdx.x >> 6);
-  if (j >= V.Np) return;
+  const int j0 = (lb - p * gridDim.x) * kColsPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCPW;
   WaveLds& W = wl[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
-  Line<KPL> L;
-  L.load_lanes(K.hc + (size_t)p * kstride + (size_t)j * kSR, (size_t)ldc * kSR, V.Mp);
-  const LineCells<false> keyf{V, j};
-  float th, Tc;
-  Group c_lo, c_hi;
-  c_lo.g = c_hi.g = -1;
   unsigned hint = kNoHint;
-  line_threshold(L, V.Mp, kappa, keyf, W, &c_lo, &c_hi, &th, &Tc, &hint);
-  if (lane == 0) {
-    thr[(size_t)p * thr_stride + j] = th;
-    Tq[(size_t)p * thr_stride + j] = Tc;
-  }
-  const size_t w = (size_t)p * mask_stride + (size_t)lane * ld + j;
+  const int jend = min(j0 + kCPW, V.Np);
+  // the next column's line is loaded while this one is searched (its HBM latency hidden)
+  auto load_col = [&](Line<KPL>& Ld, int j) {
+    int64_t coloff = (int64_t)p * kstride + (int64_t)j * kSR;
+    asm volatile("" : "+s"(coloff));  // per-column address: nothing per lane hoisted out of the loop
+    Ld.load_lanes(K.hc + coloff, (size_t)ldc * kSR, V.Mp);
+  };
+  Line<KPL> Lnext;
+  if (j0 < jend) load_col(Lnext, j0);
+#pragma unroll 1
+  for (int j = j0; j < jend; ++j) {
+    const Line<KPL> L = Lnext;
+    if (j + 1 < jend) load_col(Lnext, j + 1);
+    const LineCells<false> keyf{V, j};
+    float th, Tc;
+    Group c_lo, c_hi;
+    c_lo.g = c_hi.g = -1;
+    line_threshold(L, V.Mp, kappa, keyf, W, &c_lo, &c_hi, &th, &Tc, &hint);
+    if (lane == 0) {
+      thr[(size_t)p * thr_stride + j] = th;
+      Tq[(size_t)p * thr_stride + j] = Tc;
+    }
+    const size_t w = (size_t)p * mask_stride + (size_t)lane * ld + j;
 #ifdef ACOSS_ABL_NOLEBITS
-  const uint32_t bits = 0;
+    const uint32_t bits = 0;
 #else
-  const uint32_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
+    const uint32_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
 #endif
-  if (lane * KPL >= V.Mp) return;
-  maskT[w] = bits & RT[w];
+    if (lane * KPL < V.Mp) maskT[w] = bits & RT[w];
+  }
 }
 
 }  // namespace
@@ -1036,7 +1109,7 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
     prof_end(PH_SEL_ROWS, s);
   }
   prof_begin(PH_SEL_COLS, s);
-  hipLaunchKernelGGL(k_sel_cols9, dim3((L + 3) / 4, nb), dim3(256), 0, s, B, K, ldk, kstride, kappa, RT, thr_c, T_c,
+  hipLaunchKernelGGL(k_sel_cols9, dim3((L + kColsPerBlock - 1) / kColsPerBlock, nb), dim3(256), 0, s, B, K, ldk, kstride, kappa, RT, thr_c, T_c,
                      thr_stride, maskT, mask_stride, ld);
   ACOSS_LAUNCH_CHECK();
   prof_end(PH_SEL_COLS, s);

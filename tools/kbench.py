@@ -23,6 +23,7 @@ ap.add_argument("--pairs", type=int, default=4000)
 ap.add_argument("--frames", type=int, default=2000)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--dmax", action="store_true")
+ap.add_argument("--noprof", action="store_true", help="no per-phase events: plain wall time per call")
 a = ap.parse_args()
 tracks, labels = corpus_tracks(1, a.frames, 20250101)
 bank = ChromaBank(tracks)
@@ -30,13 +31,13 @@ T = len(tracks)
 pairs = np.array([(i, j) for i in range(T) for j in range(i + 1, T)], np.int32)[: a.pairs]
 pt = torch.as_tensor(pairs).cuda()
 for r in range(a.reps):
-    _lib.profile_enable(True)
+    _lib.profile_enable(not a.noprof)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     out = bank.crp_align(pt, qmax=True, dmax=a.dmax)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    ph = _lib.profile_read()
+    ph = {} if a.noprof else _lib.profile_read()
     _lib.profile_enable(False)
     print("rep %d: %.1f pairs/s  %s" % (r, len(pairs) / dt, {k: round(v[0] / v[1], 3) for k, v in ph.items()}))
 print("qmax checksum", float(out["qmax"].double().sum()))
