@@ -29,6 +29,21 @@ namespace {
 
 constexpr int kMS = 9;
 
+#ifdef ACOSS_STAMPS  // diagnostic builds only: per-phase cycle sums of the fused sweep
+__device__ unsigned long long d_sweep_stamps[16];
+__device__ __forceinline__ unsigned long long sstamp() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#define ACOSS_STAMP(v) const unsigned long long v = sstamp()
+#define ACOSS_STAMP_ADD(slot, a, b) \
+  if ((threadIdx.x & 63) == 0) atomicAdd(&d_sweep_stamps[slot], (b) - (a))
+#else
+#define ACOSS_STAMP(v)
+#define ACOSS_STAMP_ADD(slot, a, b)
+#endif
+
 struct PairView {
   const float* X;   // query frames
   const float* X2;  // query frame pairs (f, f + 1) interleaved bin by bin (24 floats per f)
@@ -90,6 +105,9 @@ struct KeyPlanes {
 // frame pair (cell_gram), sequential 9-term sum, d2 = (NX_i - 2 dot) + NY_j clamped at +0
 // (cell_finish). Valid cells only (i < M', j < N'): every frame is inside its track.
 __device__ __forceinline__ float cell_gram(const PairView& V, int fq, int fr) {
+#ifdef ACOSS_ABL_NOGRAM  // timing ablation only (wrong results): no frame loads in the recompute
+  return (float)(fq * 3 + fr);
+#endif
   const f32x4* x = reinterpret_cast<const f32x4*>(V.X + (size_t)fq * 12);
   const f32x4* y = reinterpret_cast<const f32x4*>(V.Yr + (size_t)fr * 12);
   const f32x4 x0 = x[0], x1 = x[1], x2 = x[2], y0 = y[0], y1 = y[1], y2 = y[2];
@@ -232,13 +250,20 @@ __device__ __forceinline__ void diag_pk(const PairView& V, int i0, int td, int j
     for (int b = 1; b < 12; ++b) g = __builtin_fmaf(xb[b].x, yb[b].y, g);
     G[0] = g;
   }
+  // software pipeline: step kk + 2's query pair (SMEM) and pair block (LDS) are requested as
+  // soon as step kk's chain has consumed its operands, so their latency overlaps the emits
+  xpair(PAR, xb);
+  yblock(td + PAR, yb);
 #pragma unroll
   for (int kk = PAR; kk + 1 < kSteps; kk += 2) {
-    xpair(kk, xb);
-    yblock(td + kk, yb);
     f32x2 g = pk_fma(xb[0], yb[0], f32x2{0.0f, 0.0f});
 #pragma unroll
     for (int b = 1; b < 12; ++b) g = pk_fma(xb[b], yb[b], g);
+    if (kk + 3 < kSteps) {
+      xpair(kk + 2, xb);
+      yblock(td + kk + 2, yb);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     G[kk] = g.x;
     G[kk + 1] = g.y;
     // rows completed by this pair: r = kk - 8 and kk - 7
@@ -323,6 +348,7 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
   };
   if (FAST) fetch(-(kSR - 1));
   for (int j0 = -(kSR - 1); j0 < V.Np; j0 += kSW) {
+    ACOSS_STAMP(t0);
     __syncthreads();
     if (FAST) {  // pair blocks for diag_pk: Ys[f/2][bin][f&1] (tau == 1)
 #pragma unroll
@@ -357,6 +383,7 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
       }
     }
     __syncthreads();
+    ACOSS_STAMP(t1);
     if (FAST) {
       if (j0 + kSW < V.Np) fetch(j0 + kSW);
       const int w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
@@ -423,7 +450,9 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
       }
     }
     }  // !FAST
+    ACOSS_STAMP(t2);
     __syncthreads();
+    ACOSS_STAMP(t3);
     // columns [j0, j0 + 256) complete: column-major prefixes, 32 rows = 64 B per column
     const int jj = j0 + t;
     if (jj >= 0 && jj < V.Np) {
@@ -444,6 +473,13 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
     for (int e = t; e < (kSR - 1) * (kTP / 2); e += kSW) {
       const int c = e / (kTP / 2), w = e - c * (kTP / 2);
       reinterpret_cast<uint32_t*>(tileT)[c * (kTP / 2) + w] = reinterpret_cast<const uint32_t*>(tileT)[(kSW + c) * (kTP / 2) + w];
+    }
+    ACOSS_STAMP(t4);
+    if (FAST) {
+      ACOSS_STAMP_ADD(0, t0, t1);  // fill + 2 barriers
+      ACOSS_STAMP_ADD(1, t1, t2);  // diagonal walk
+      ACOSS_STAMP_ADD(2, t2, t3);  // barrier after the walk
+      ACOSS_STAMP_ADD(3, t3, t4);  // column-plane stores, barrier, roll
     }
   }
 }
@@ -533,6 +569,29 @@ struct Line {
     for (int h = 0; h < KPL / 2; ++h) c = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c;
     return wave_sum((int)c);
 #endif
+  }
+  // Bit q set iff element q's prefix == P (P <= 0x7f80). Per field, (a ^ P) + 0x7fff keeps bit
+  // 15 iff a != P; fields are <= 0x7fff, so nothing carries across. Elements past KPL: 0.
+  __device__ __forceinline__ uint32_t eq_mask(unsigned P) const {
+    const unsigned PP = P * 0x10001u;
+    uint32_t ne = 0;
+#pragma unroll
+    for (int h = 0; h < KPL / 2; ++h) {
+      const unsigned s = (pv[h] ^ PP) + 0x7fff7fffu;
+      ne |= (((s >> 15) & 1u) << (2 * h)) | ((s >> 31) << (2 * h + 1));
+    }
+    return KPL >= 32 ? ~ne : ~ne & ((1u << KPL) - 1u);
+  }
+  // Bit q set iff element q's prefix <= x (x <= 0x7fff; kNone is never <= a real x).
+  __device__ __forceinline__ uint32_t le_mask(unsigned x) const {
+    const unsigned X2 = (x + 0x8000u) * 0x10001u;
+    uint32_t le = 0;
+#pragma unroll
+    for (int h = 0; h < KPL / 2; ++h) {
+      const unsigned s = X2 - pv[h];
+      le |= (((s >> 15) & 1u) << (2 * h)) | ((s >> 31) << (2 * h + 1));
+    }
+    return le;
   }
   // min over elements (kNone is above every real prefix) and max over real elements
   // (kNone + 1 wraps to 0x8000, masked to 0: below every real prefix + 1)
@@ -628,15 +687,14 @@ __device__ Group group_keys(const Line<KPL>& L, unsigned P, int g, const KF& key
   const int lane = threadIdx.x & 63;
   int ebase = lane * KPL;  // opaque: element indices are not hoisted out of callers' loops
   asm volatile("" : "+v"(ebase));
-  int base = 0;
-#pragma unroll
-  for (int q = 0; q < KPL; ++q) {
-    const bool m = L.pfx(q) == P;
-    const unsigned long long bal = __ballot(m);
-    if (m)
-      W.list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] =
-          ebase + q;
-    base += __popcll(bal);
+  // member list: per-lane SWAR member mask, one wave scan for the lane's first slot, then each
+  // lane writes its own members (usually 0-2 per lane; no per-element ballot)
+  uint32_t m = L.eq_mask(P);
+  const int cnt = __builtin_popcount(m);
+  int idx = wave_incl_scan(cnt) - cnt;
+  while (m) {
+    W.list[idx++] = ebase + __builtin_ctz(m);
+    m &= m - 1;
   }
   __builtin_amdgcn_wave_barrier();
   // the 9 g Gram terms, one per lane and round (about 2 rounds for a typical group of 10-15)
@@ -697,9 +755,7 @@ __device__ __forceinline__ void group_rank2(const Group& G, int rho, unsigned* v
 template <int KPL, class F>
 __device__ void group_rounds(const Line<KPL>& L, unsigned P, int g, WaveLds& W, F fn) {
   const int lane = threadIdx.x & 63;
-  uint32_t m = 0;
-#pragma unroll
-  for (int q = 0; q < KPL; ++q) m |= (uint32_t)(L.pfx(q) == P) << q;
+  uint32_t m = L.eq_mask(P);
   const int cnt = __builtin_popcount(m);
   int idx = wave_incl_scan(cnt) - cnt;
   int ebase = lane * KPL;
@@ -840,15 +896,9 @@ __device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, 
                             const Group& c_hi) {
   const unsigned T16 = Tbits >> 16;
   const int lane = threadIdx.x & 63;
-  uint32_t word = 0;
-  int amb = 0;
-#pragma unroll
-  for (int q = 0; q < KPL; ++q) {
-    const unsigned k = L.pfx(q);  // kNone is never <= T16 (T16 <= 0x7f80)
-    word |= (uint32_t)(k < T16) << q;
-    amb += k == T16;
-  }
-  const int g = wave_sum(amb);
+  // k < T16 and k == T16 as SWAR masks (kNone is never <= T16 <= 0x7f80)
+  const uint32_t word = T16 ? L.le_mask(T16 - 1) : 0u;
+  const int g = wave_sum(__builtin_popcount(L.eq_mask(T16)));
   if (g == 0) return word;
   if (g <= 64) {
     Group G;
@@ -1005,12 +1055,16 @@ __global__ __launch_bounds__(256, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K,
     sweep_body<true>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
   else
     sweep_body<false>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
+  ACOSS_STAMP(r0);
   __syncthreads();  // the strip's F rows are complete (block-scope visibility of the global stores)
 #ifdef ACOSS_ABL_NOROWS  // timing ablation only (wrong results): sweep without the row select
   return;
 #endif
   rows_body<4>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld,
                reinterpret_cast<WaveLds*>(smem), reinterpret_cast<uint32_t(*)[64]>(smem + 4 * sizeof(WaveLds)));
+  ACOSS_STAMP(r1);
+  ACOSS_STAMP_ADD(4, r0, r1);  // row select
+  if (threadIdx.x == 0) ACOSS_STAMP_ADD(5, 0ull, 1ull);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1117,3 +1171,14 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
 }
 
 }  // namespace acoss
+
+#ifdef ACOSS_STAMPS
+extern "C" int acoss_debug_sweep_stamps(unsigned long long* out16) {
+  if (hipDeviceSynchronize() != hipSuccess) return ACOSS_E_HIP;
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(acoss::d_sweep_stamps), 16 * sizeof(unsigned long long)) != hipSuccess)
+    return ACOSS_E_HIP;
+  unsigned long long z[16] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(acoss::d_sweep_stamps), z, sizeof(z)) != hipSuccess) return ACOSS_E_HIP;
+  return ACOSS_OK;
+}
+#endif
