@@ -39,7 +39,10 @@ __device__ __forceinline__ unsigned long long sstamp() {
 #define ACOSS_STAMP(v) const unsigned long long v = sstamp()
 #define ACOSS_STAMP_ADD(slot, a, b) \
   if ((threadIdx.x & 63) == 0) atomicAdd(&d_sweep_stamps[slot], (b) - (a))
+#define ACOSS_COUNT(slot, v) \
+  if ((threadIdx.x & 63) == 0) atomicAdd(&d_sweep_stamps[slot], (unsigned long long)(v))
 #else
+#define ACOSS_COUNT(slot, v)
 #define ACOSS_STAMP(v)
 #define ACOSS_STAMP_ADD(slot, a, b)
 #endif
@@ -143,6 +146,7 @@ __device__ __forceinline__ unsigned cell_key(const PairView& V, int i, int j) {
 // pair's pointers by value (a reference to the kernel's PairView would put it on the stack).
 template <bool ROW>
 struct LineCells {
+  static constexpr bool kRow = ROW;
   PairView V;
   int fix;
   __device__ __forceinline__ int qi(int e) const { return ROW ? fix : e; }
@@ -628,7 +632,7 @@ constexpr unsigned kNoHint = 0xffffffffu;
 
 template <int KPL>
 __device__ __forceinline__ unsigned prefix_of_rank(const Line<KPL>& L, int rho, unsigned a, unsigned b, int n,
-                                                   unsigned hint, int* le_out, int* less_out) {
+                                                   unsigned hint, int* le_out, int* less_out, int* passes) {
   int c_b = n;    // count(<= b): every element is <= kmax
   int c_am1 = 0;  // count(<= a - 1): none is below kmin
   // one count per iteration, probe chosen by the mode (a single count_le site keeps the
@@ -646,6 +650,7 @@ __device__ __forceinline__ unsigned prefix_of_rank(const Line<KPL>& L, int rho, 
     else
       t = (a + b) >> 1;
     const int c = L.count_le(t);
+    ++*passes;
     const bool greater = c > rho;
     if (greater) {
       b = t;
@@ -697,13 +702,15 @@ __device__ Group group_keys(const Line<KPL>& L, unsigned P, int g, const KF& key
     m &= m - 1;
   }
   __builtin_amdgcn_wave_barrier();
-  // the 9 g Gram terms, one per lane and round (about 2 rounds for a typical group of 10-15)
+  // the 9 g Gram terms, one per lane and round (about 2 rounds for a typical group of 8-9)
   for (int t = lane; t < kMS * g; t += 64) {
     const int k = t / kMS, u = t - k * kMS;
     const int e = W.list[k];
     W.gv[t] = cell_gram(keyf.V, (keyf.qi(e) + u) * keyf.V.tau, (keyf.rj(e) + u) * keyf.V.tau);
   }
   __builtin_amdgcn_wave_barrier();
+  ACOSS_COUNT(KF::kRow ? 8 : 13, 1);
+  ACOSS_COUNT(KF::kRow ? 9 : 14, g);
   Group G;
   G.P = P;
   G.g = g;
@@ -851,7 +858,10 @@ __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF&
   unsigned kmin = 0, kmax = 0x7f80u;  // every real prefix (finite non-negative float) is <= 0x7f80
   if (*hint == kNoHint) L.min_max(&kmin, &kmax);
   int le, less;
-  const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, *hint, &le, &less);
+  int passes = 0;
+  const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, *hint, &le, &less, &passes);
+  ACOSS_COUNT(KF::kRow ? 6 : 11, 1);
+  ACOSS_COUNT(KF::kRow ? 7 : 12, passes);
   *hint = Pl;
   unsigned vlo, vhi;
 #ifdef ACOSS_ABL_NOGROUP
@@ -907,7 +917,10 @@ __device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, 
     else if (c_hi.g >= 0 && c_hi.P == T16)
       G = c_hi;
     else
+    {
+      ACOSS_COUNT(KF::kRow ? 10 : 15, 1);
       G = group_keys(L, T16, g, keyf, W);
+    }
     W.words[lane] = 0u;
     __builtin_amdgcn_wave_barrier();
     if (lane < G.g && G.key <= Tbits) atomicOr(&W.words[G.elem / KPL], 1u << (G.elem % KPL));
