@@ -605,6 +605,163 @@ __global__ __launch_bounds__(64) void k_crp_dp(const uint32_t* __restrict__ mask
   if (lane == 0) out[p] = best;
 }
 
+// --------------------------------------------------------------------------------------
+// k_crp_dp_pk<ALIGN>: k_crp_dp<ALIGN, true, 32> in packed 16-bit integers. With
+// gamma_open == gamma_ext = K/2 (K a small integer, 1 for the reference's 0.5), every score is
+// a multiple of 1/2, so 2Q is an exact integer below 4 L: lane l keeps rows (h, h + 16) of a
+// column in one u32 (row h low, row h + 16 high) and takes two rows per v_pk_max_u16 /
+// v_pk_add_u16 / saturating v_pk_sub_u16 (max(x - K, 0) in one instruction). The predecessor
+// rows of pair h are pair h - 1 / h - 2 of the previous columns; pairs 0 and 1 splice in the
+// rows handed down by the lane above (v_perm). Bit-identical to the f32 kernel: both compute
+// the same exact multiples of 1/2 (the f32 values never round).
+// --------------------------------------------------------------------------------------
+typedef unsigned short dp_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pk16(dp_u16x2 v) { return __builtin_bit_cast(unsigned, v); }
+__device__ __forceinline__ dp_u16x2 up16(unsigned v) { return __builtin_bit_cast(dp_u16x2, v); }
+__device__ __forceinline__ unsigned pk_max16(unsigned a, unsigned b) { return pk16(__builtin_elementwise_max(up16(a), up16(b))); }
+__device__ __forceinline__ unsigned pk_add16(unsigned a, unsigned b) { return pk16(up16(a) + up16(b)); }
+__device__ __forceinline__ unsigned pk_sub16(unsigned a, unsigned b) { return pk16(up16(a) - up16(b)); }
+__device__ __forceinline__ unsigned pk_subsat16(unsigned a, unsigned b) {
+  return pk16(__builtin_elementwise_sub_sat(up16(a), up16(b)));
+}
+
+struct DpAbovePk {  // what lane l-1 (or the band above) hands down for one column
+  unsigned hq;      // its rows 30 (low half) and 31 (high half), x2 units
+  uint32_t b;       // bit0 = C[row 30], bit1 = C[row 31]
+};
+
+template <int ALIGN>
+struct DpLanePk {
+  unsigned K;          // gamma in x2 units, both halves
+  int Np;
+  uint32_t rz0, rz1;   // AND masks of pairs 0 / 1: rows 0 and 1 of the first band are 0
+  uint32_t w1, w2;     // CRP words of columns c-1, c-2
+  DpAbovePk h1, h2;    // from above for columns c-1, c-2
+  unsigned best;
+
+  __device__ __forceinline__ DpAbovePk step(unsigned (&pn)[16], const unsigned (&p1)[16], const unsigned (&p2)[16],
+                                            uint32_t w0, const DpAbovePk& h0, int c) {
+    const bool colok = (c >= 2) && (c < Np);
+    // rows (-1, 15) and (-2, 14) of column c-1, (-1, 15) of column c-2
+    const unsigned a0 = __builtin_amdgcn_perm(p1[15], h1.hq, 0x05040302u);
+    const unsigned b0 = __builtin_amdgcn_perm(p1[14], h1.hq, 0x05040100u);
+    const unsigned c0 = __builtin_amdgcn_perm(p2[15], h2.hq, 0x05040302u);
+#pragma unroll
+    for (int h = 0; h < 16; ++h) {
+      const unsigned A = h >= 1 ? p1[h - 1] : a0;                  // Q[r-1][c-1]
+      unsigned B = h >= 2 ? p1[h - 2] : (h == 1 ? a0 : b0);        // Q[r-2][c-1]
+      unsigned Cq = h >= 1 ? p2[h - 1] : c0;                       // Q[r-1][c-2]
+      if (ALIGN == 1) {
+        const unsigned cb = h >= 1 ? (w0 >> (h - 1)) & 0x10001u : ((h0.b >> 1) & 1u) | (((w0 >> 15) & 1u) << 16);
+        B = pk_add16(B, cb << 1);                                  // + C[r-1][c]
+        Cq = pk_add16(Cq, ((w1 >> h) & 0x10001u) << 1);            // + C[r][c-1]
+      }
+      const unsigned mx = pk_max16(pk_max16(A, B), Cq);
+      const unsigned m = pk_sub16(0u, (w0 >> h) & 0x10001u);      // 0xffff where C[r][c] = 1
+      unsigned v = (m & pk_add16(mx, 0x00020002u)) | (~m & pk_subsat16(mx, K));
+      if (h == 0) v &= rz0;
+      if (h == 1) v &= rz1;
+      v = colok ? v : 0u;
+      best = pk_max16(best, v);
+      pn[h] = v;
+    }
+    DpAbovePk out;
+    out.hq = __builtin_amdgcn_perm(pn[15], pn[14], 0x07060302u);
+    out.b = (w0 >> 30) & 3u;
+    h2 = h1;
+    h1 = h0;
+    w2 = w1;
+    w1 = w0;
+    return out;
+  }
+};
+
+template <int ALIGN>
+__global__ __launch_bounds__(64) void k_crp_dp_pk(const uint32_t* __restrict__ maskT, int64_t mask_stride, int ld,
+                                                  const int2* __restrict__ dims, unsigned K,
+                                                  float4* __restrict__ bnd, int64_t bnd_stride,
+                                                  float* __restrict__ out) {
+  const int p = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int2 dm = dims[p];
+  const int Mp = dm.x, Np = dm.y;
+  unsigned best = 0u;
+  constexpr int kBand = 64 * 32;
+  const int nbands = (Mp + kBand - 1) / kBand;
+  for (int band = 0; band < nbands; ++band) {
+    const int row0 = band * kBand + lane * 32;
+    const uint32_t* mrow = maskT + (size_t)p * mask_stride + (size_t)(row0 >> 5) * ld;
+    float4* bout = bnd + (size_t)p * bnd_stride + (size_t)band * ld;
+    const float4* bin = bnd + (size_t)p * bnd_stride + (size_t)(band - 1) * ld;
+    DpLanePk<ALIGN> L;
+    L.K = K * 0x10001u;
+    L.Np = Np;
+    L.rz0 = row0 == 0 ? 0xffff0000u : 0xffffffffu;
+    L.rz1 = L.rz0;
+    L.w1 = L.w2 = 0;
+    L.h1 = L.h2 = DpAbovePk{0u, 0u};
+    L.best = 0u;
+    unsigned qa[16], qb[16], qc[16];
+#pragma unroll
+    for (int h = 0; h < 16; ++h) qa[h] = qb[h] = qc[h] = 0u;
+    DpAbovePk pub{0u, 0u};
+    const int S_end = Np + 63;
+    const bool lane_active = row0 < Mp;
+    auto fetch = [&](int c) -> uint32_t { return (lane_active && c >= 0 && c < Np) ? mrow[c] : 0u; };
+    auto recv = [&](const DpAbovePk& mine, int c) -> DpAbovePk {
+      DpAbovePk h;
+      h.hq = (unsigned)__shfl_up((int)mine.hq, 1);
+      h.b = (uint32_t)__shfl_up((int)mine.b, 1);
+      if (lane == 0) {
+        if (band > 0 && c >= 0 && c < Np) {
+          const float4 v = bin[c];
+          h = DpAbovePk{__builtin_bit_cast(unsigned, v.x), __builtin_bit_cast(unsigned, v.y)};
+        } else {
+          h = DpAbovePk{0u, 0u};
+        }
+      }
+      return h;
+    };
+    auto publish = [&](const DpAbovePk& o, int c) {
+      if (lane == 63 && band + 1 < nbands && c >= 0 && c < Np)
+        bout[c] = make_float4(__builtin_bit_cast(float, o.hq), __builtin_bit_cast(float, o.b), 0.0f, 0.0f);
+    };
+    uint32_t wnext = fetch(-lane);
+    for (int s = 0; s < S_end; s += 3) {
+      {
+        const int c = s - lane;
+        const uint32_t w0 = wnext;
+        wnext = fetch(c + 1);
+        const DpAbovePk h0 = recv(pub, c);
+        pub = L.step(qa, qb, qc, w0, h0, c);
+        publish(pub, c);
+      }
+      if (s + 1 < S_end) {
+        const int c = s + 1 - lane;
+        const uint32_t w0 = wnext;
+        wnext = fetch(c + 1);
+        const DpAbovePk h0 = recv(pub, c);
+        pub = L.step(qc, qa, qb, w0, h0, c);
+        publish(pub, c);
+      }
+      if (s + 2 < S_end) {
+        const int c = s + 2 - lane;
+        const uint32_t w0 = wnext;
+        wnext = fetch(c + 1);
+        const DpAbovePk h0 = recv(pub, c);
+        pub = L.step(qb, qc, qa, w0, h0, c);
+        publish(pub, c);
+      }
+    }
+    best = pk_max16(best, L.best);
+    __threadfence_block();
+    __syncthreads();
+  }
+  const unsigned b2 = max(best & 0xffffu, best >> 16);
+  const float r = wave_max(0.5f * (float)b2);
+  if (lane == 0) out[p] = r;
+}
+
 // Dense (M x N) uint8 CRP <-> strip words maskT[i/32][j] (bit i%32).
 __global__ void k_unpack_mask(const uint32_t* __restrict__ maskT, int ld, int M, int N, uint8_t* __restrict__ C) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -699,6 +856,14 @@ void launch_dp_r(bool eqg, int nb, const uint32_t* maskT, int64_t mstride, int l
                        bstride, out);
 }
 
+// The packed 16-bit DP (k_crp_dp_pk) is exact when gamma_open == gamma_ext is a multiple of 1/2
+// and every doubled score fits 16 bits: scores grow by at most 2 per column (chen17), so 2Q < 4L.
+inline bool dp_packed_ok(bool eqg, int L, float go) {
+  static const bool off = getenv("ACOSS_DP_F32") != nullptr;
+  const float k2 = 2.0f * go;
+  return !off && eqg && L <= 16000 && k2 >= 0.0f && k2 <= 1024.0f && k2 == floorf(k2);
+}
+
 // Rows per lane from the batch's longest CRP (L rows): every choice below 2048 rows is one band,
 // so the band-boundary buffer (ceil(L / 2048) bands) always suffices.
 template <int ALIGN>
@@ -708,6 +873,9 @@ void launch_dp(bool eqg, int nb, int L, const uint32_t* maskT, int64_t mstride, 
     launch_dp_r<ALIGN, 8>(eqg, nb, maskT, mstride, ld, dims, go, ge, bnd, bstride, out, s);
   else if (L <= 1024)
     launch_dp_r<ALIGN, 16>(eqg, nb, maskT, mstride, ld, dims, go, ge, bnd, bstride, out, s);
+  else if (ALIGN == 1 && dp_packed_ok(eqg, L, go))
+    hipLaunchKernelGGL(k_crp_dp_pk<ALIGN>, dim3(nb), dim3(64), 0, s, maskT, mstride, ld, dims, (unsigned)(2.0f * go), bnd,
+                       bstride, out);
   else
     launch_dp_r<ALIGN, 32>(eqg, nb, maskT, mstride, ld, dims, go, ge, bnd, bstride, out, s);
 }
@@ -831,7 +999,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   // Infinity Cache.
   const size_t slot = 4 + 8 + 4 * (size_t)thr_stride * 4 + 4 * (size_t)mask_stride + 16 * (size_t)bnd_stride +
                       4 * (size_t)yrot_stride;
-  size_t budget = (size_t)8 << 30;  // DP batch scratch: ~13k pairs at 2000 frames in one DP launch
+  size_t budget = (size_t)16 << 30;  // DP batch scratch: ~25k pairs at 2000 frames in one DP launch
   if (const char* e = getenv("ACOSS_WS_BYTES")) budget = strtoull(e, nullptr, 10);
   int64_t nbmax = (int64_t)(budget / slot);
   if (const char* e = getenv("ACOSS_BATCH_PAIRS")) nbmax = atoll(e);

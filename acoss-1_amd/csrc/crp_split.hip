@@ -532,23 +532,27 @@ struct Line {
   __device__ __forceinline__ void load_lanes(const uint16_t* col0, size_t lane_stride, int n) {
     const int lane = threadIdx.x & 63;
     const int base = lane * KPL;
-    const uint16_t* src = col0 + (size_t)lane * lane_stride;
-    if (base + KPL <= n) {
+    // every lane loads a whole run: the lane holding the end of the line reads its run in full
+    // (runs lie inside the plane: the row pitch and the strips are whole runs) and masks the
+    // tail; lanes past the line re-read lane 0's run and mask all of it. No per-element
+    // conditional loads: hipcc branches around each and waits vmcnt(0) after each (16-32
+    // serial L2 round trips per line)
+    const uint16_t* src = col0 + (base < n ? (size_t)lane * lane_stride : (size_t)0);
 #pragma unroll
-      for (int q = 0; q < KPL / 8; ++q) {
-        const uint4 w = reinterpret_cast<const uint4*>(src)[q];
-        pv[4 * q + 0] = w.x;
-        pv[4 * q + 1] = w.y;
-        pv[4 * q + 2] = w.z;
-        pv[4 * q + 3] = w.w;
-      }
-    } else {
+    for (int q = 0; q < KPL / 8; ++q) {
+      const uint4 w = reinterpret_cast<const uint4*>(src)[q];
+      pv[4 * q + 0] = w.x;
+      pv[4 * q + 1] = w.y;
+      pv[4 * q + 2] = w.z;
+      pv[4 * q + 3] = w.w;
+    }
+    if (base + KPL > n) {
       int nv = n - base;  // opaque per call: no hoisted per-element predicates in callers' loops
       asm volatile("" : "+v"(nv));
 #pragma unroll
       for (int h = 0; h < KPL / 2; ++h) {
-        const unsigned a = (2 * h < nv) ? (unsigned)src[2 * h] : kNone;
-        const unsigned b = (2 * h + 1 < nv) ? (unsigned)src[2 * h + 1] : kNone;
+        const unsigned a = (2 * h < nv) ? (pv[h] & 0xffffu) : kNone;
+        const unsigned b = (2 * h + 1 < nv) ? (pv[h] >> 16) : kNone;
         pv[h] = a | (b << 16);
       }
     }
@@ -702,6 +706,10 @@ __device__ Group group_keys(const Line<KPL>& L, unsigned P, int g, const KF& key
     m &= m - 1;
   }
   __builtin_amdgcn_wave_barrier();
+  // this lane's member (lanes >= g take member 0: a valid cell) and its two stacked norms,
+  // requested before the Gram rounds so that their latency overlaps them
+  const int e_me = W.list[lane < g ? lane : 0];
+  const float nq_me = keyf.V.NXq[keyf.qi(e_me)], nr_me = keyf.V.NXr[keyf.rj(e_me)];
   // the 9 g Gram terms, one per lane and round (about 2 rounds for a typical group of 8-9)
   for (int t = lane; t < kMS * g; t += 64) {
     const int k = t / kMS, u = t - k * kMS;
@@ -714,13 +722,14 @@ __device__ Group group_keys(const Line<KPL>& L, unsigned P, int g, const KF& key
   Group G;
   G.P = P;
   G.g = g;
-  G.elem = lane < g ? W.list[lane] : 0;
+  G.elem = lane < g ? e_me : 0;
   G.key = 0xffffffffu;
   if (lane < g) {
     float dot = W.gv[lane * kMS];
 #pragma unroll
     for (int u = 1; u < kMS; ++u) dot = dot + W.gv[lane * kMS + u];
-    G.key = cell_finish(keyf.V, keyf.qi(G.elem), keyf.rj(G.elem), dot);
+    const float d2 = (nq_me - 2.0f * dot) + nr_me;  // cell_finish with the preloaded norms
+    G.key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
   }
   __builtin_amdgcn_wave_barrier();
   return G;
@@ -1116,12 +1125,22 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
     asm volatile("" : "+s"(coloff));  // per-column address: nothing per lane hoisted out of the loop
     Ld.load_lanes(K.hc + coloff, (size_t)ldc * kSR, V.Mp);
   };
+#ifdef ACOSS_COLS_NOPF  // no next-column prefetch: 16 VGPRs fewer (occupancy over latency)
+#pragma unroll 1
+  for (int j = j0; j < jend; ++j) {
+    Line<KPL> L;
+    load_col(L, j);
+#else
   Line<KPL> Lnext;
   if (j0 < jend) load_col(Lnext, j0);
 #pragma unroll 1
   for (int j = j0; j < jend; ++j) {
     const Line<KPL> L = Lnext;
     if (j + 1 < jend) load_col(Lnext, j + 1);
+#endif
+    // this column's row-threshold word, requested now and used after the select
+    const size_t w = (size_t)p * mask_stride + (size_t)(lane * KPL < V.Mp ? lane : 0) * ld + j;
+    const uint32_t rt = RT[w];
     const LineCells<false> keyf{V, j};
     float th, Tc;
     Group c_lo, c_hi;
@@ -1131,13 +1150,12 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
       thr[(size_t)p * thr_stride + j] = th;
       Tq[(size_t)p * thr_stride + j] = Tc;
     }
-    const size_t w = (size_t)p * mask_stride + (size_t)lane * ld + j;
 #ifdef ACOSS_ABL_NOLEBITS
     const uint32_t bits = 0;
 #else
     const uint32_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
 #endif
-    if (lane * KPL < V.Mp) maskT[w] = bits & RT[w];
+    if (lane * KPL < V.Mp) maskT[w] = bits & rt;
   }
 }
 
