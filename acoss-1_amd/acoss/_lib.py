@@ -44,6 +44,7 @@ SIGNATURES = {
     "acoss_get_oti": [_vp, _vp, _i32, _vp, _vp],
     "acoss_binarize_rows": [_vp, _i32, _i32, _i32, _vp, _vp],
     "acoss_wcsm": [_vp, _i32, _i32, _i32, _i32, _f32, _vp, _vp],
+    "acoss_snf_step": [_vp, _i32, _i32, _i32, _vp, _vp, _i32, ctypes.c_double, _vp, _vp],
     "acoss_simple_mp": [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _vp],
     "acoss_median_downsample": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
     "acoss_simple_features": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _i64, _vp],
@@ -292,6 +293,30 @@ def wcsm(CSM, k1, k2, mu=0.5):
     out = torch.empty(C.shape, dtype=torch.float32, device="cuda")
     rc = lib.acoss_wcsm(_ptr(C), int(C.shape[0]), int(C.shape[1]), int(k1), int(k2), float(mu), _ptr(out), _stream())
     _check(rc, "acoss_wcsm")
+    return out
+
+
+def snf_step(mats, skip, J, V, reg_diag, out=None):
+    """One doSimilarityFusionWs cross-diffusion step for matrix `skip`
+    (similarity_fusion.py:163-174): S . mean_{m != skip}(mats[m]) . S^T + reg_diag * I.
+    mats: list of (n, n) float64 device tensors; J (n, K) column indices, V (n, K) float64
+    row-normalised kNN weights of S. Returns a new (n, n) float64 device tensor (or `out`)."""
+    torch = _torch()
+    lib = load_library()
+    n = int(mats[0].shape[0])
+    for m in mats:
+        if m.dtype != torch.float64 or not m.is_cuda or tuple(m.shape) != (n, n) or not m.is_contiguous():
+            raise ValueError("snf_step: every matrix must be a contiguous (n, n) float64 device tensor")
+    Jd = _dev(J, torch.int32).contiguous()
+    Vd = _dev(V, torch.float64).contiguous()
+    if Jd.shape != Vd.shape or Jd.dim() != 2 or Jd.shape[0] != n:
+        raise ValueError("snf_step: J and V must both be (n, K)")
+    if out is None:
+        out = torch.empty((n, n), dtype=torch.float64, device=mats[0].device)
+    ptrs = (ctypes.c_void_p * len(mats))(*[m.data_ptr() for m in mats])
+    rc = lib.acoss_snf_step(ptrs, len(mats), int(skip), n, _ptr(Jd), _ptr(Vd), int(Jd.shape[1]), float(reg_diag),
+                            _ptr(out), _stream())
+    _check(rc, "acoss_snf_step")
     return out
 
 

@@ -1,9 +1,9 @@
 """Similarity network fusion (acoss/algorithms/utils/similarity_fusion.py) on the GPU.
 
 Same functions and arguments as the reference; numpy in, numpy out, device tensors inside.
-`getWCSM` runs the HIP kernel (misc.hip); the N x N fusion runs as device tensor ops: the
-kNN sets come from torch.topk, and the sparse S . P . S^T products are row gathers
-(S holds K entries per row), so an iteration is O(N^2 K), not a dense N^3 GEMM.
+`getWCSM` runs the HIP kernel (misc.hip); each cross-diffusion step S . P . S^T runs as the HIP
+kernels of snf.hip (acoss_snf_step: two row-sparse products, O(N^2 K), not a dense N^3 GEMM,
+summed in scipy's csr order). W, P and the kNN sets (torch.topk) are one-off device tensor ops.
 
 Two reference behaviours are kept on purpose:
   * dtypes follow numpy's: float32 inputs give float32 W/P, the diffusion runs in float64;
@@ -101,20 +101,6 @@ class _KNN:
     def __init__(self, J, V, n):
         self.J, self.V, self.n = J, V, n
 
-    def dot(self, X, chunk_bytes=1 << 29):
-        """S . X for dense X (n x m), in float64 like scipy's csr(float32) . ndarray(float64)."""
-        torch = _lib._torch()
-        X = X.to(torch.float64)
-        out = torch.empty((self.n, X.shape[1]), dtype=torch.float64, device=X.device)
-        K = self.J.shape[1]
-        rows = max(1, int(chunk_bytes // max(1, K * X.shape[1] * 8)))
-        Vd = self.V.to(torch.float64)
-        for r0 in range(0, self.n, rows):
-            r1 = min(self.n, r0 + rows)
-            g = X[self.J[r0:r1].reshape(-1)].reshape(r1 - r0, K, X.shape[1])
-            out[r0:r1] = torch.einsum("rk,rkm->rm", Vd[r0:r1], g)
-        return out
-
     def todense(self):
         torch = _lib._torch()
         S = torch.zeros((self.n, self.n), dtype=self.V.dtype, device=self.V.device)
@@ -143,23 +129,20 @@ def _fusion_ws(Ws, K=5, niters=20, reg_diag=1):
     torch = _lib._torch()
     Ps = [_getP(W) for W in Ws]
     Ss = [_getS(W, K) for W in Ws]
-    Pts = [P.clone() for P in Ps]
-    nextPts = [torch.zeros(P.shape, dtype=torch.float64, device=P.device) for P in Pts]
+    # float32 P upcast once (exact): in the reference the first iteration adds the float32 Ps
+    # into float64 accumulators, every later one adds float64 matrices
+    Pts = [P.to(torch.float64).contiguous() for P in Ps]
     N = len(Pts)
-    pix = torch.arange(Ws[0].shape[0], device=Ws[0].device)
+    if N < 2:
+        raise ValueError("doSimilarityFusionWs needs at least two matrices")
     for it in range(niters):
+        # the reference's `Pts = nextPts` aliasing: from the second iteration on, matrix i's
+        # update already sees the new matrices k < i; replacing Pts[i] in place of the list
+        # entry reproduces that, and the first iteration (separate lists) sees only old ones
+        nxt = list(Pts) if it == 0 else Pts
         for i in range(N):
-            nextPts[i] *= 0
-            for k in range(N):
-                if i == k:
-                    continue
-                nextPts[i] += Pts[k]
-            nextPts[i] /= float(N - 1)
-            # S . P . S^T as in the reference: S.dot((S.dot(P.T)).T)
-            nextPts[i] = Ss[i].dot(Ss[i].dot(nextPts[i].T).T)
-            if reg_diag > 0:
-                nextPts[i][pix, pix] += reg_diag
-        Pts = nextPts
+            nxt[i] = _lib.snf_step(Pts, i, Ss[i].J, Ss[i].V, reg_diag)
+        Pts = nxt
     Fused = torch.zeros(Pts[0].shape, dtype=torch.float64, device=Pts[0].device)
     for Pt in Pts:
         Fused += Pt

@@ -1,0 +1,172 @@
+// Similarity network fusion, cross-diffusion step (f2; acoss/algorithms/utils/similarity_fusion.py:146-186).
+//
+// One step of doSimilarityFusionWs for matrix i:
+//   A   = (sum_{m != i} Pts[m]) / (L - 1)                    (similarity_fusion.py:165-169)
+//   out = S_i . ((S_i . A^T)^T) + reg_diag * I                 (:171-174)
+// with S_i the kNN-truncated, row-normalised W_i (getS, :121-143): K entries per row.
+// (S A^T)^T = A S^T, so the step is two row-sparse products:
+//   B[a, j]   = sum_k V[j,k] * A[a, J[j,k]]   (k_snf_right: column gather inside row a)
+//   out[i, j] = sum_k V[i,k] * B[J[i,k], j]   (k_snf_left: K coalesced row reads of B)
+// Both sum over k in ascending column order from 0, one rounded multiply and one rounded add
+// per term (-ffp-contract=off), as scipy's csr_matvecs does on the csr matrix that getS builds
+// (coo -> csr sorts the column indices). A is never materialised: the average is formed at the
+// gather, in the reference's order (m ascending, then one division). All arithmetic is float64.
+//
+// Traffic per step (n x n float64): k_snf_right reads the L-1 matrices once (row a of each stays
+// L2-resident while 256 columns gather from it) and writes B once; k_snf_left reads K rows of B
+// per output row (the hub rows repeat and hit L2) and writes out once. HBM-bound: about
+// (L + 2 + K) * 8 * n^2 bytes at worst, (L + 2) * 8 * n^2 when B's gathered rows stay in L2.
+#include "common.hpp"
+
+namespace acoss {
+namespace {
+
+constexpr int kSnfMaxMats = 8;
+constexpr int kSnfMaxK = 64;
+constexpr int kSnfRowsPerBlock = 8;  // k_snf_right: rows a per block (share one J/V column tile)
+
+struct MatPtrs {
+  const double* p[kSnfMaxMats];
+};
+
+// Per row: the K (column, value) pairs sorted by column (insertion sort; K <= 64, rows
+// have no repeated columns), so both products sum in csr order.
+__global__ void k_snf_sort_knn(const int32_t* __restrict__ J, const double* __restrict__ V, int32_t n, int32_t K,
+                               int32_t* __restrict__ Js, double* __restrict__ Vs) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  int32_t jj[kSnfMaxK];
+  double vv[kSnfMaxK];
+  for (int k = 0; k < K; ++k) {
+    int32_t c = J[(int64_t)r * K + k];
+    double v = V[(int64_t)r * K + k];
+    int q = k;
+    while (q > 0 && jj[q - 1] > c) {
+      jj[q] = jj[q - 1];
+      vv[q] = vv[q - 1];
+      --q;
+    }
+    jj[q] = c;
+    vv[q] = v;
+  }
+  for (int k = 0; k < K; ++k) {
+    Js[(int64_t)r * K + k] = jj[k];
+    Vs[(int64_t)r * K + k] = vv[k];
+  }
+}
+
+// B[a, j] = sum_k Vs[j,k] * A[a, Js[j,k]], A = average of the L-1 matrices other than `skip`.
+// Block = 256 consecutive columns j x kSnfRowsPerBlock rows a; blockIdx.x runs over column tiles
+// fastest, so the blocks resident on an XCD gather from the same few rows of A in its L2.
+__global__ __launch_bounds__(256) void k_snf_right(MatPtrs mats, int32_t n_mats, int32_t skip, int32_t n, int32_t K,
+                                                   const int32_t* __restrict__ Js, const double* __restrict__ Vs,
+                                                   double* __restrict__ B) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int a0 = blockIdx.y * kSnfRowsPerBlock;
+  if (j >= n) return;
+  const double denom = (double)(n_mats - 1);
+  double acc[kSnfRowsPerBlock];
+#pragma unroll
+  for (int r = 0; r < kSnfRowsPerBlock; ++r) acc[r] = 0.0;
+  for (int k = 0; k < K; ++k) {
+    const int32_t c = Js[(int64_t)j * K + k];
+    const double v = Vs[(int64_t)j * K + k];
+#pragma unroll
+    for (int r = 0; r < kSnfRowsPerBlock; ++r) {
+      const int a = a0 + r;
+      if (a < n) {
+        const int64_t e = (int64_t)a * n + c;
+        double s = 0.0;
+        for (int m = 0; m < n_mats; ++m) {
+          if (m == skip) continue;
+          s = s + mats.p[m][e];
+        }
+        s = s / denom;
+        acc[r] = acc[r] + v * s;
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kSnfRowsPerBlock; ++r) {
+    const int a = a0 + r;
+    if (a < n) B[(int64_t)a * n + j] = acc[r];
+  }
+}
+
+// out[i, j] = sum_k Vs[i,k] * B[Js[i,k], j] (+ reg_diag on the diagonal, added after the sum
+// as the reference's separate `nextPts[i][pix, pix] += reg_diag`). Block = row i x 1024 columns,
+// 4 consecutive columns per thread as two 16-byte loads per gathered row.
+__global__ __launch_bounds__(256) void k_snf_left(const double* __restrict__ B, int32_t n, int32_t K,
+                                                  const int32_t* __restrict__ Js, const double* __restrict__ Vs,
+                                                  double reg_diag, double* __restrict__ out) {
+  const int i = blockIdx.y;
+  const int j0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (j0 >= n) return;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  const bool full = (j0 + 4 <= n) && ((n & 1) == 0);
+  for (int k = 0; k < K; ++k) {
+    const int32_t row = Js[(int64_t)i * K + k];
+    const double v = Vs[(int64_t)i * K + k];
+    const double* src = B + (int64_t)row * n + j0;
+    if (full) {
+      const double2 x0 = *reinterpret_cast<const double2*>(src);
+      const double2 x1 = *reinterpret_cast<const double2*>(src + 2);
+      acc[0] = acc[0] + v * x0.x;
+      acc[1] = acc[1] + v * x0.y;
+      acc[2] = acc[2] + v * x1.x;
+      acc[3] = acc[3] + v * x1.y;
+    } else {
+      for (int t = 0; t < 4; ++t)
+        if (j0 + t < n) acc[t] = acc[t] + v * src[t];
+    }
+  }
+  double* dst = out + (int64_t)i * n + j0;
+  for (int t = 0; t < 4; ++t) {
+    const int j = j0 + t;
+    if (j < n) {
+      double x = acc[t];
+      if (j == i && reg_diag > 0.0) x = x + reg_diag;
+      dst[t] = x;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace acoss
+
+using namespace acoss;
+
+extern "C" int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t skip, int32_t n,
+                              const int32_t* J, const double* V, int32_t K, double reg_diag, double* out,
+                              void* hip_stream) {
+  clear_error();
+  if (!mats || n_mats < 2 || n_mats > kSnfMaxMats || skip < 0 || skip >= n_mats || n <= 0 || !J || !V || !out ||
+      K <= 0 || K > kSnfMaxK || K > n) {
+    set_error("acoss_snf_step: bad arguments (need 2 <= n_mats <= %d, 0 < K <= min(n, %d))", kSnfMaxMats, kSnfMaxK);
+    return ACOSS_E_ARG;
+  }
+  MatPtrs mp{};
+  for (int m = 0; m < n_mats; ++m) {
+    if (!mats[m] || (m != skip && mats[m] == out)) {
+      set_error("acoss_snf_step: matrix %d is NULL or aliases the output", m);
+      return ACOSS_E_ARG;
+    }
+    mp.p[m] = mats[m];
+  }
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  const size_t nn = (size_t)n * n;
+  const size_t knn = align_up((size_t)n * K, 64);
+  char* ws = static_cast<char*>(workspace(12, nn * 8 + knn * 12 + 512));
+  if (!ws) return ACOSS_E_HIP;
+  double* Bm = reinterpret_cast<double*>(ws);
+  double* Vs = reinterpret_cast<double*>(ws + nn * 8);
+  int32_t* Js = reinterpret_cast<int32_t*>(ws + nn * 8 + knn * 8);
+  hipLaunchKernelGGL(k_snf_sort_knn, dim3((n + 255) / 256), dim3(256), 0, s, J, V, n, K, Js, Vs);
+  ACOSS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_snf_right, dim3((n + 255) / 256, (n + kSnfRowsPerBlock - 1) / kSnfRowsPerBlock), dim3(256), 0, s,
+                     mp, n_mats, skip, n, K, Js, Vs, Bm);
+  ACOSS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_snf_left, dim3((n + 1023) / 1024, n), dim3(256), 0, s, Bm, n, K, Js, Vs, reg_diag, out);
+  ACOSS_LAUNCH_CHECK();
+  return ACOSS_OK;
+}

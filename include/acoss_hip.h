@@ -117,6 +117,16 @@ int acoss_binarize_rows(const float* D, int32_t M, int32_t N, int32_t nneighbs, 
 int acoss_wcsm(const float* CSM, int32_t M, int32_t N, int32_t k1, int32_t k2, float mu, float* W,
                void* hip_stream);
 
+/* One cross-diffusion step of similarity network fusion for matrix `skip` (f2, replaces the body
+ * of the loop at acoss/algorithms/utils/similarity_fusion.py:163-174 in doSimilarityFusionWs):
+ *   out = S . A . S^T + reg_diag * I,  A = (sum_{m != skip} mats[m]) / (n_mats - 1),
+ * S the kNN-truncated row-normalised affinity (getS, :121-143) given as J (n x K) int32 column
+ * indices and V (n x K) float64 values, any order within a row (sums run in ascending column
+ * order, as scipy's csr product). mats: HOST array of n_mats device pointers to (n x n) float64
+ * matrices; out (n x n) float64 may alias mats[skip] but no other. 2 <= n_mats <= 8, K <= 64. */
+int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t skip, int32_t n, const int32_t* J,
+                   const double* V, int32_t K, double reg_diag, double* out, void* hip_stream);
+
 /* SiMPle matrix profile score (A11, acoss/algorithms/simple_silva.py:68-118) for a batch of
  * ordered pairs, including the per-pair OTI roll of the reference (Simple.oti, :45-54).
  * feats: packed (12 x n_t) float64 blocks, track t at element offset track_off[t] (dim-major,

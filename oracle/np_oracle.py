@@ -107,3 +107,23 @@ def simple_oti(seq_a, seq_b):
     v = np.array([np.dot(pa, np.roll(pb, i)) for i in range(12)])
     k = int(np.argsort(v, kind="stable")[-1])
     return np.roll(seq_b, k, axis=0), k
+
+
+def snf_step(mats, skip, J, V, reg_diag):
+    """One cross-diffusion step of doSimilarityFusionWs for matrix `skip`
+    (acoss/algorithms/utils/similarity_fusion.py:163-174): the average of the other matrices,
+    then S.dot((S.dot(A.T)).T) with S the csr matrix getS builds from (J, V) (:137-142),
+    then reg_diag added on the diagonal. float64 throughout, as the reference from its second
+    iteration on."""
+    from scipy import sparse
+    n, K = J.shape
+    A = np.zeros((n, n))
+    for k, M in enumerate(mats):
+        if k != skip:
+            A += M
+    A /= float(len(mats) - 1)
+    S = sparse.coo_matrix((V.ravel(), (np.repeat(np.arange(n), K), J.ravel())), shape=(n, n)).tocsr()
+    out = S.dot((S.dot(A.T)).T)
+    if reg_diag > 0:
+        out[np.arange(n), np.arange(n)] += reg_diag
+    return out

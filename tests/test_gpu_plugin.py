@@ -158,3 +158,32 @@ def test_earlyfusion_composition(tmp_path, monkeypatch):
                 assert ef.Ds[key][i, j] == np.float32(ref), (i, j, key)  # Ds is float32, like the memmap
     ef.do_late_fusion()
     assert np.all(np.isfinite(ef.Ds["late"])) and np.all(np.isfinite(ef.Ds["early+late"]))
+
+
+@pytest.mark.parametrize("n,K,L", [(40, 5, 2), (333, 20, 3), (1030, 7, 4)])
+def test_snf_step_bitexact(n, K, L):
+    """acoss_snf_step vs the reference's own scipy expression (np_oracle.snf_step): the HIP
+    kernels sum in csr column order with unfused multiply/add, so the result is bit-exact."""
+    import torch
+    rng = np.random.default_rng(n)
+    mats = [rng.random((n, n)) for _ in range(L)]
+    J = np.stack([rng.choice(n, K, replace=False) for _ in range(n)]).astype(np.int32)
+    V = rng.random((n, K)).astype(np.float32)
+    V = (V / V.sum(1, keepdims=True)).astype(np.float64)
+    dm = [torch.as_tensor(m).cuda() for m in mats]
+    for skip in range(L):
+        got = _lib.snf_step(dm, skip, J, V, 1.0).cpu().numpy()
+        np.testing.assert_array_equal(got, npo.snf_step(mats, skip, J, V, 1.0))
+    got = _lib.snf_step(dm, 0, J, V, 0.0).cpu().numpy()
+    np.testing.assert_array_equal(got, npo.snf_step(mats, 0, J, V, 0.0))
+
+
+def test_snf_step_rejects_bad_args():
+    import torch
+    m = torch.zeros((8, 8), dtype=torch.float64, device="cuda")
+    J = np.zeros((8, 2), np.int32)
+    V = np.zeros((8, 2))
+    with pytest.raises(_lib.AcossHipError):
+        _lib.snf_step([m], 0, J, V, 1.0)  # one matrix: nothing to average
+    with pytest.raises(ValueError):
+        _lib.snf_step([m, m.float()], 0, J, V, 1.0)

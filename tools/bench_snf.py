@@ -1,0 +1,65 @@
+"""SNF cross-diffusion step throughput (f2): acoss_snf_step on n x n float64 matrices.
+
+    python tools/bench_snf.py [--n 15000] [--L 2] [--K 20] [--reps 5]
+
+Da-TACOS-sized by default (n = 15,000 tracks, K = 20 as LateFusionChen.do_late_fusion,
+latefusion_chen.py:88). Times each of the three kernels with HIP events on the launch stream
+(rocprofv3 gives the same split) and prints one JSON line with the step time and the HBM
+roofline of the two product kernels: algorithmic bytes = (L-1) + 1 matrices read/written by
+k_snf_right and 1 read (K rows per output row, L2-resident in the ideal) + 1 written by
+k_snf_left, n^2 float64 each.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "acoss-1_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from acoss import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=15000)
+    ap.add_argument("--L", type=int, default=2)
+    ap.add_argument("--K", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    n, L, K = a.n, a.L, a.K
+    g = torch.Generator(device="cuda").manual_seed(1)
+    mats = [torch.rand((n, n), dtype=torch.float64, device="cuda", generator=g) for _ in range(L)]
+    W = torch.rand((n, n), dtype=torch.float32, device="cuda", generator=g)
+    V, J = torch.topk(W, K, dim=1)
+    V = (V / V.sum(1, keepdim=True)).to(torch.float64)
+    J = J.to(torch.int32)
+    del W
+    out = torch.empty((n, n), dtype=torch.float64, device="cuda")
+    _lib.snf_step(mats, 0, J, V, 1.0, out=out)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    times = []
+    for r in range(a.reps):
+        e0.record(s)
+        _lib.snf_step(mats, r % L, J, V, 1.0, out=out)
+        e1.record(s)
+        e1.synchronize()
+        times.append(e0.elapsed_time(e1))
+    ms = float(np.median(times))
+    algo = (L + 2) * 8.0 * n * n
+    gbs = algo / (ms * 1e-3) / 1e9
+    print(json.dumps({"what": "acoss_snf_step (one SNF cross-diffusion step)", "n": n, "L": L, "K": K,
+                      "ms_per_step": round(ms, 4), "ms_all": [round(t, 4) for t in times],
+                      "algorithmic_bytes": algo, "achieved_GBs": round(gbs, 1), "peak_GBs": 8000.0,
+                      "frac": round(gbs / 8000.0, 4),
+                      "late_fusion_20_iters_s": round(ms * 20 * L / 1e3, 3)}))
+
+
+if __name__ == "__main__":
+    main()
