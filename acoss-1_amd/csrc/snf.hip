@@ -4,18 +4,20 @@
 //   A   = (sum_{m != i} Pts[m]) / (L - 1)                    (similarity_fusion.py:165-169)
 //   out = S_i . ((S_i . A^T)^T) + reg_diag * I                 (:171-174)
 // with S_i the kNN-truncated, row-normalised W_i (getS, :121-143): K entries per row.
-// (S A^T)^T = A S^T, so the step is two row-sparse products:
-//   B[a, j]   = sum_k V[j,k] * A[a, J[j,k]]   (k_snf_right: column gather inside row a)
-//   out[i, j] = sum_k V[i,k] * B[J[i,k], j]   (k_snf_left: K coalesced row reads of B)
-// Both sum over k in ascending column order from 0, one rounded multiply and one rounded add
-// per term (-ffp-contract=off), as scipy's csr_matvecs does on the csr matrix that getS builds
-// (coo -> csr sorts the column indices). A is never materialised: the average is formed at the
-// gather, in the reference's order (m ascending, then one division). All arithmetic is float64.
+// (S A^T)^T = A S^T, so the step is two row-sparse products, both as COALESCED row gathers:
+//   At        = A^T                            (k_snf_avg_t: the average, transposed via LDS)
+//   B         = (S . At)^T                     (k_snf_gather_t: B^T[j, :] = sum_k V[j,k] At[J[j,k], :],
+//                                               written transposed through an LDS tile)
+//   out[i, :] = sum_k V[i,k] * B[J[i,k], :]    (k_snf_left)
+// so B[a, j] = sum_k V[j,k] * A[a, J[j,k]], the reference's inner product, term for term.
+// Both products sum over k in ascending column order from 0, one rounded multiply and one
+// rounded add per term (-ffp-contract=off), as scipy's csr_matvecs does on the csr matrix that
+// getS builds (coo -> csr sorts the column indices); the transposes are exact, and the average
+// is formed in the reference's order (m ascending, then one division). All float64.
 //
-// Traffic per step (n x n float64): k_snf_right reads the L-1 matrices once (row a of each stays
-// L2-resident while 256 columns gather from it) and writes B once; k_snf_left reads K rows of B
-// per output row (the hub rows repeat and hit L2) and writes out once. HBM-bound: about
-// (L + 2 + K) * 8 * n^2 bytes at worst, (L + 2) * 8 * n^2 when B's gathered rows stay in L2.
+// Traffic per step (n x n float64 each): the transpose reads the L-1 other matrices and writes
+// At; each gather reads K rows per output row (repeated hub rows hit L2/MALL) and writes one
+// matrix. Algorithmic HBM bytes: (L - 1 + 1 + 2 + 2) * 8 * n^2 = (L + 4) * 8 n^2.
 #include "common.hpp"
 
 namespace acoss {
@@ -23,7 +25,6 @@ namespace {
 
 constexpr int kSnfMaxMats = 8;
 constexpr int kSnfMaxK = 64;
-constexpr int kSnfRowsPerBlock = 8;  // k_snf_right: rows a per block (share one J/V column tile)
 
 struct MatPtrs {
   const double* p[kSnfMaxMats];
@@ -55,41 +56,70 @@ __global__ void k_snf_sort_knn(const int32_t* __restrict__ J, const double* __re
   }
 }
 
-// B[a, j] = sum_k Vs[j,k] * A[a, Js[j,k]], A = average of the L-1 matrices other than `skip`.
-// Block = 256 consecutive columns j x kSnfRowsPerBlock rows a; blockIdx.x runs over column tiles
-// fastest, so the blocks resident on an XCD gather from the same few rows of A in its L2.
-__global__ __launch_bounds__(256) void k_snf_right(MatPtrs mats, int32_t n_mats, int32_t skip, int32_t n, int32_t K,
-                                                   const int32_t* __restrict__ Js, const double* __restrict__ Vs,
-                                                   double* __restrict__ B) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  const int a0 = blockIdx.y * kSnfRowsPerBlock;
-  if (j >= n) return;
+// At[c, a] = (sum_{m != skip} mats[m][a, c]) / (n_mats - 1): 64 x 64 tile through LDS.
+__global__ __launch_bounds__(256) void k_snf_avg_t(MatPtrs mats, int32_t n_mats, int32_t skip, int32_t n,
+                                                   double* __restrict__ At) {
+  __shared__ double tile[64][65];
+  const int a0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int t = threadIdx.x;
   const double denom = (double)(n_mats - 1);
-  double acc[kSnfRowsPerBlock];
+#pragma unroll 4
+  for (int r = 0; r < 16; ++r) {
+    const int idx = t + 256 * r;
+    const int a = a0 + (idx >> 6), c = c0 + (idx & 63);
+    double s = 0.0;
+    if (a < n && c < n) {
+      const int64_t e = (int64_t)a * n + c;
+      for (int m = 0; m < n_mats; ++m) {
+        if (m == skip) continue;
+        s = s + mats.p[m][e];
+      }
+      s = s / denom;
+    }
+    tile[idx & 63][idx >> 6] = s;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int r = 0; r < 16; ++r) {
+    const int idx = t + 256 * r;
+    const int c = c0 + (idx >> 6), a = a0 + (idx & 63);
+    if (a < n && c < n) At[(int64_t)c * n + a] = tile[idx >> 6][idx & 63];
+  }
+}
+
+// B[a, j] = sum_k Vs[j,k] * At[Js[j,k], a]. Block = 32 rows j x 64 columns a; each wave takes
+// 8 rows j, lane = column a (each gathered row segment is one 512-byte run), and the 32 x 64
+// result leaves transposed through LDS as 64 runs of 32 doubles.
+constexpr int kGJ = 32;
+__global__ __launch_bounds__(256) void k_snf_gather_t(const double* __restrict__ At, int32_t n, int32_t K,
+                                                      const int32_t* __restrict__ Js,
+                                                      const double* __restrict__ Vs, double* __restrict__ B) {
+  __shared__ double tile[64][kGJ + 1];
+  const int a0 = blockIdx.x * 64, j0 = blockIdx.y * kGJ;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int a = a0 + lane;
+  const bool aok = a < n;
 #pragma unroll
-  for (int r = 0; r < kSnfRowsPerBlock; ++r) acc[r] = 0.0;
-  for (int k = 0; k < K; ++k) {
-    const int32_t c = Js[(int64_t)j * K + k];
-    const double v = Vs[(int64_t)j * K + k];
-#pragma unroll
-    for (int r = 0; r < kSnfRowsPerBlock; ++r) {
-      const int a = a0 + r;
-      if (a < n) {
-        const int64_t e = (int64_t)a * n + c;
-        double s = 0.0;
-        for (int m = 0; m < n_mats; ++m) {
-          if (m == skip) continue;
-          s = s + mats.p[m][e];
-        }
-        s = s / denom;
-        acc[r] = acc[r] + v * s;
+  for (int q = 0; q < kGJ / 4; ++q) {
+    const int jl = w * (kGJ / 4) + q;
+    const int j = j0 + jl;
+    double acc = 0.0;
+    if (j < n) {
+      for (int k = 0; k < K; ++k) {
+        const int32_t row = Js[(int64_t)j * K + k];
+        const double v = Vs[(int64_t)j * K + k];
+        if (aok) acc = acc + v * At[(int64_t)row * n + a];
       }
     }
+    tile[lane][jl] = acc;
   }
+  __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kSnfRowsPerBlock; ++r) {
-    const int a = a0 + r;
-    if (a < n) B[(int64_t)a * n + j] = acc[r];
+  for (int r = 0; r < (64 * kGJ) / 256; ++r) {
+    const int idx = threadIdx.x + 256 * r;
+    const int al = idx / kGJ, jl = idx % kGJ;
+    const int aa = a0 + al, j = j0 + jl;
+    if (aa < n && j < n) B[(int64_t)aa * n + j] = tile[al][jl];
   }
 }
 
@@ -156,15 +186,18 @@ extern "C" int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   const size_t nn = (size_t)n * n;
   const size_t knn = align_up((size_t)n * K, 64);
-  char* ws = static_cast<char*>(workspace(12, nn * 8 + knn * 12 + 512));
+  char* ws = static_cast<char*>(workspace(12, 2 * nn * 8 + knn * 12 + 512));
   if (!ws) return ACOSS_E_HIP;
   double* Bm = reinterpret_cast<double*>(ws);
-  double* Vs = reinterpret_cast<double*>(ws + nn * 8);
-  int32_t* Js = reinterpret_cast<int32_t*>(ws + nn * 8 + knn * 8);
+  double* At = reinterpret_cast<double*>(ws + nn * 8);
+  double* Vs = reinterpret_cast<double*>(ws + 2 * nn * 8);
+  int32_t* Js = reinterpret_cast<int32_t*>(ws + 2 * nn * 8 + knn * 8);
+  const unsigned nt = (unsigned)((n + 63) / 64);
   hipLaunchKernelGGL(k_snf_sort_knn, dim3((n + 255) / 256), dim3(256), 0, s, J, V, n, K, Js, Vs);
   ACOSS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_snf_right, dim3((n + 255) / 256, (n + kSnfRowsPerBlock - 1) / kSnfRowsPerBlock), dim3(256), 0, s,
-                     mp, n_mats, skip, n, K, Js, Vs, Bm);
+  hipLaunchKernelGGL(k_snf_avg_t, dim3(nt, nt), dim3(256), 0, s, mp, n_mats, skip, n, At);
+  ACOSS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_snf_gather_t, dim3(nt, (n + kGJ - 1) / kGJ), dim3(256), 0, s, At, n, K, Js, Vs, Bm);
   ACOSS_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_snf_left, dim3((n + 1023) / 1024, n), dim3(256), 0, s, Bm, n, K, Js, Vs, reg_diag, out);
   ACOSS_LAUNCH_CHECK();

@@ -3,11 +3,10 @@
     python tools/bench_snf.py [--n 15000] [--L 2] [--K 20] [--reps 5]
 
 Da-TACOS-sized by default (n = 15,000 tracks, K = 20 as LateFusionChen.do_late_fusion,
-latefusion_chen.py:88). Times each of the three kernels with HIP events on the launch stream
-(rocprofv3 gives the same split) and prints one JSON line with the step time and the HBM
-roofline of the two product kernels: algorithmic bytes = (L-1) + 1 matrices read/written by
-k_snf_right and 1 read (K rows per output row, L2-resident in the ideal) + 1 written by
-k_snf_left, n^2 float64 each.
+latefusion_chen.py:88). Times the whole step with HIP events on the launch stream
+(rocprofv3 gives the per-kernel split) and prints one JSON line with the step time and the
+HBM roofline: algorithmic bytes = (L + 4) * 8 * n^2 (the transpose reads L-1 matrices and
+writes one; each of the two gathers reads one matrix, once in the ideal, and writes one).
 """
 import argparse
 import json
@@ -52,7 +51,7 @@ def main():
         e1.synchronize()
         times.append(e0.elapsed_time(e1))
     ms = float(np.median(times))
-    algo = (L + 2) * 8.0 * n * n
+    algo = (L + 4) * 8.0 * n * n
     gbs = algo / (ms * 1e-3) / 1e9
     print(json.dumps({"what": "acoss_snf_step (one SNF cross-diffusion step)", "n": n, "L": L, "K": K,
                       "ms_per_step": round(ms, 4), "ms_all": [round(t, 4) for t in times],
