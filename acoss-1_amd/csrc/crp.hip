@@ -454,7 +454,13 @@ struct DpAbove {  // what lane l-1 (or the band above) hands down for one column
   uint32_t b;      // bit0 = C[row R-2], bit1 = C[row R-1]
 };
 
-template <int ALIGN, bool EQG, int R>
+// FAST (serra09 with gamma_open == gamma_ext = K/2 >= 0, the reference's setting): every score is
+// an exact multiple of 1/2, so "hit ? mx + 1 : max(mx - go, 0)" is max(fma(hit, 1 + go, mx - go), 0)
+// exactly, and the validity masks move out of the row loop: the kernel zeroes the CRP words of
+// columns < 2 and rows outside [2, Mp) at the fetch. Cells there then hold 0 (top-left: all their
+// predecessors are 0) or at most max(0, best - go) (bottom/right: no hit, and they never feed a
+// valid cell), so neither the valid scores nor their maximum change.
+template <int ALIGN, bool EQG, int R, bool FAST = false>
 struct DpLane {
   float go, ge;
   int Np, lane, c_off;  // column of this lane at step s: s - lane
@@ -475,6 +481,19 @@ struct DpLane {
     const uint64_t e0 = ((uint64_t)w0 << 2) | h0.b;
     const uint64_t e1 = ((uint64_t)w1 << 2) | h1.b;
     const uint64_t e2 = ((uint64_t)w2 << 2) | h2.b;
+    if constexpr (FAST) {
+      const float g1 = 1.0f + go;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float Qa = r >= 1 ? q1[r - 1] : h1.q31;
+        const float Qb = r >= 2 ? q1[r - 2] : (r == 1 ? h1.q31 : h1.q30);
+        const float Qc = r >= 1 ? q2[r - 1] : h2.q31;
+        const float mx = fmaxf(fmaxf(Qa, Qb), Qc);
+        const float t = fmaf((float)((w0 >> r) & 1u), g1, mx - go);
+        best = fmaxf(best, t);
+        qn[r] = fmaxf(t, 0.0f);
+      }
+    } else {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const float Qa = r >= 1 ? q1[r - 1] : h1.q31;                            // Q[r-1][c-1]
@@ -500,6 +519,7 @@ struct DpLane {
       best = fmaxf(best, v);
       qn[r] = v;
     }
+    }
     DpAbove out;
     out.q30 = qn[R - 2];
     out.q31 = qn[R - 1];
@@ -512,8 +532,8 @@ struct DpLane {
   }
 };
 
-template <int ALIGN, bool EQG, int R>
-__global__ __launch_bounds__(64) void k_crp_dp(const uint32_t* __restrict__ maskT, int64_t mask_stride, int ld,
+template <int ALIGN, bool EQG, int R, bool FAST>
+__device__ __forceinline__ void crp_dp_body(const uint32_t* __restrict__ maskT, int64_t mask_stride, int ld,
                                                const int2* __restrict__ dims, float go, float ge,
                                                float4* __restrict__ bnd, int64_t bnd_stride,
                                                float* __restrict__ out) {
@@ -530,7 +550,7 @@ __global__ __launch_bounds__(64) void k_crp_dp(const uint32_t* __restrict__ mask
     const int sh = row0 & 31;  // this lane's R rows inside its 32-row strip word
     float4* bout = bnd + (size_t)p * bnd_stride + (size_t)band * ld;
     const float4* bin = bnd + (size_t)p * bnd_stride + (size_t)(band - 1) * ld;
-    DpLane<ALIGN, EQG, R> L;
+    DpLane<ALIGN, EQG, R, FAST> L;
     L.go = go;
     L.ge = ge;
     L.Np = Np;
@@ -548,9 +568,10 @@ __global__ __launch_bounds__(64) void k_crp_dp(const uint32_t* __restrict__ mask
     const int S_end = Np + 63;
     const bool lane_active = row0 < Mp;
     auto fetch = [&](int c) -> uint32_t {
-      if (!(lane_active && c >= 0 && c < Np)) return 0u;
+      if (!(lane_active && c >= (FAST ? 2 : 0) && c < Np)) return 0u;
       const uint32_t w = mrow[c];
-      return R == 32 ? w : (w >> sh) & ((1u << (R & 31)) - 1u);
+      const uint32_t wr = R == 32 ? w : (w >> sh) & ((1u << (R & 31)) - 1u);
+      return FAST ? (wr & rv) : wr;
     };
     auto recv = [&](const DpAbove& mine, int c) -> DpAbove {
       DpAbove h;
@@ -603,6 +624,23 @@ __global__ __launch_bounds__(64) void k_crp_dp(const uint32_t* __restrict__ mask
   }
   best = wave_max(best);
   if (lane == 0) out[p] = best;
+}
+
+template <int ALIGN, bool EQG, int R>
+__global__ __launch_bounds__(64) void k_crp_dp(const uint32_t* __restrict__ maskT, int64_t mask_stride, int ld,
+                                               const int2* __restrict__ dims, float go, float ge,
+                                               float4* __restrict__ bnd, int64_t bnd_stride,
+                                               float* __restrict__ out) {
+  crp_dp_body<ALIGN, EQG, R, false>(maskT, mask_stride, ld, dims, go, ge, bnd, bnd_stride, out);
+}
+
+// No occupancy hint: the FAST body compiles to about 200 VGPRs (2 waves per SIMD), which measured
+// faster than forcing it into 128 (4 waves per SIMD): 14.2 vs 14.8 ms per covers80 step.
+template <int R>
+__global__ __launch_bounds__(64) void k_crp_dp_fast(
+    const uint32_t* __restrict__ maskT, int64_t mask_stride, int ld, const int2* __restrict__ dims, float go, float ge,
+    float4* __restrict__ bnd, int64_t bnd_stride, float* __restrict__ out) {
+  crp_dp_body<0, true, R, true>(maskT, mask_stride, ld, dims, go, ge, bnd, bnd_stride, out);
 }
 
 // --------------------------------------------------------------------------------------
@@ -848,7 +886,12 @@ int prepare_stage(int m, int ld, Stage* st) {
 template <int ALIGN, int R>
 void launch_dp_r(bool eqg, int nb, const uint32_t* maskT, int64_t mstride, int ld, const int2* dims, float go,
                  float ge, float4* bnd, int64_t bstride, float* out, hipStream_t s) {
-  if (eqg)
+  const float k2 = 2.0f * go;
+  static const bool no_fast = getenv("ACOSS_DP_NOFAST") != nullptr;
+  if (ALIGN == 0 && eqg && !no_fast && k2 >= 0.0f && k2 <= 1024.0f && k2 == floorf(k2))
+    hipLaunchKernelGGL((k_crp_dp_fast<R>), dim3(nb), dim3(64), 0, s, maskT, mstride, ld, dims, go, ge,
+                       bnd, bstride, out);
+  else if (eqg)
     hipLaunchKernelGGL((k_crp_dp<ALIGN, true, R>), dim3(nb), dim3(64), 0, s, maskT, mstride, ld, dims, go, ge, bnd,
                        bstride, out);
   else
