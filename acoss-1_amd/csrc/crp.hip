@@ -460,6 +460,27 @@ struct DpAbove {  // what lane l-1 (or the band above) hands down for one column
 // columns < 2 and rows outside [2, Mp) at the fetch. Cells there then hold 0 (top-left: all their
 // predecessors are 0) or at most max(0, best - go) (bottom/right: no hit, and they never feed a
 // valid cell), so neither the valid scores nor their maximum change.
+// v_cvt_f32_ubyteB: byte B of v as a float (the compiler emits only the byte-0 form plus shifts).
+template <int B>
+__device__ __forceinline__ float cvt_f32_ubyte(uint32_t v) {
+  float f;
+  if constexpr (B == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(f) : "v"(v));
+  else if constexpr (B == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(f) : "v"(v));
+  else if constexpr (B == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(f) : "v"(v));
+  else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(f) : "v"(v));
+  return f;
+}
+
+// b is a constant after the row loops unroll, so the switch folds away
+__device__ __forceinline__ float cvt_f32_ubyte_n(uint32_t v, int b) {
+  switch (b) {
+    case 0: return cvt_f32_ubyte<0>(v);
+    case 1: return cvt_f32_ubyte<1>(v);
+    case 2: return cvt_f32_ubyte<2>(v);
+    default: return cvt_f32_ubyte<3>(v);
+  }
+}
+
 template <int ALIGN, bool EQG, int R, bool FAST = false>
 struct DpLane {
   float go, ge;
@@ -482,16 +503,32 @@ struct DpLane {
     const uint64_t e1 = ((uint64_t)w1 << 2) | h1.b;
     const uint64_t e2 = ((uint64_t)w2 << 2) | h2.b;
     if constexpr (FAST) {
-      const float g1 = 1.0f + go;
+      // two rows per v_pk_add_f32 / v_pk_fma_f32; the hit bits as bytes (rows k, k+8, k+16, k+24
+      // of one masked word), one v_cvt_f32_ubyteN each
+      typedef float dp_f32x2 __attribute__((ext_vector_type(2)));
+      const dp_f32x2 g1 = {1.0f + go, 1.0f + go};
+      const dp_f32x2 ngo = {-go, -go};
+      uint32_t bm[R < 8 ? R : 8];
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const float Qa = r >= 1 ? q1[r - 1] : h1.q31;
-        const float Qb = r >= 2 ? q1[r - 2] : (r == 1 ? h1.q31 : h1.q30);
-        const float Qc = r >= 1 ? q2[r - 1] : h2.q31;
-        const float mx = fmaxf(fmaxf(Qa, Qb), Qc);
-        const float t = fmaf((float)((w0 >> r) & 1u), g1, mx - go);
-        best = fmaxf(best, t);
-        qn[r] = fmaxf(t, 0.0f);
+      for (int k = 0; k < (R < 8 ? R : 8); ++k) bm[k] = (w0 >> k) & 0x01010101u;
+#pragma unroll
+      for (int r = 0; r < R; r += 2) {
+        float mxs[2], hb[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int rr = r + e;
+          const float Qa = rr >= 1 ? q1[rr - 1] : h1.q31;
+          const float Qb = rr >= 2 ? q1[rr - 2] : (rr == 1 ? h1.q31 : h1.q30);
+          const float Qc = rr >= 1 ? q2[rr - 1] : h2.q31;
+          mxs[e] = fmaxf(fmaxf(Qa, Qb), Qc);
+          hb[e] = cvt_f32_ubyte_n(bm[rr & 7], rr >> 3);
+        }
+        const dp_f32x2 mx = {mxs[0], mxs[1]};
+        const dp_f32x2 hv = {hb[0], hb[1]};
+        const dp_f32x2 t = __builtin_elementwise_fma(hv, g1, mx + ngo);
+        asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(t.x), "v"(t.y));
+        qn[r] = fmaxf(t.x, 0.0f);
+        qn[r + 1] = fmaxf(t.y, 0.0f);
       }
     } else {
 #pragma unroll

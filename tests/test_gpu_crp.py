@@ -50,7 +50,11 @@ def test_crp_align_batch_matches_oracle():
 @pytest.mark.parametrize("M,N,go,ge,align", [(5, 5, 0.5, 0.5, 0), (300, 200, 0.5, 0.5, 0), (300, 200, 0.5, 0.5, 1),
                                              (2100, 90, 0.5, 0.5, 0), (2100, 90, 0.5, 0.5, 1),
                                              (4200, 70, 0.7, 0.3, 0), (4200, 70, 0.7, 0.3, 1),
-                                             (257, 4100, 1.0, 0.5, 0)])
+                                             (257, 4100, 1.0, 0.5, 0),
+                                             # the serra09 fast DP (gamma_open == gamma_ext = K/2) at each
+                                             # rows-per-lane choice (8 / 16 / 32 and two bands) and K = 0, 2, 3
+                                             (300, 200, 0.0, 0.0, 0), (700, 650, 0.5, 0.5, 0),
+                                             (1000, 1500, 1.0, 1.0, 0), (2100, 2100, 1.5, 1.5, 0)])
 def test_align_crp_matches_oracle(M, N, go, ge, align):
     rng = np.random.Generator(np.random.PCG64(M + 7 * N))
     C = (rng.random((M, N)) < 0.15).astype(np.uint8)
