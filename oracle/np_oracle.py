@@ -127,3 +127,43 @@ def snf_step(mats, skip, J, V, reg_diag):
     if reg_diag > 0:
         out[np.arange(n), np.arange(n)] += reg_diag
     return out
+
+
+def snf_fused(Ds, K=5, niters=5, reg_diag=1):
+    """doSimilarityFusion (similarity_fusion.py:15-36 getW, :98-119 getP, :121-143 getS,
+    :145-182 doSimilarityFusionWs, :184-192) restated around snf_step, including the reference's
+    `Pts = nextPts` aliasing (from the second iteration on, matrix i sees the new k < i)."""
+    Ws = []
+    for D in Ds:
+        DSym = 0.5 * (D + D.T)
+        np.fill_diagonal(DSym, 0)
+        Neighbs = np.partition(DSym, K + 1, 1)[:, 0:K + 1]
+        MeanDist = np.mean(Neighbs, 1) * float(K + 1) / float(K)
+        Eps = (MeanDist[:, None] + MeanDist[None, :] + DSym) / 3
+        Denom = 2 * (0.5 * Eps) ** 2
+        Denom[Denom == 0] = 1
+        Ws.append(np.exp(-DSym ** 2 / Denom))
+    Pts, JV = [], []
+    for W in Ws:
+        RowSum = np.sum(W, 1)
+        RowSum[RowSum == 0] = 1
+        Pts.append((W / RowSum[:, None]).astype(np.float64))
+        J = np.argpartition(-W, K, 1)[:, 0:K]
+        V = W[np.repeat(np.arange(W.shape[0]), K), J.ravel()].reshape(J.shape)
+        SNorm = np.sum(V, 1)
+        SNorm[SNorm == 0] = 1
+        JV.append((J, (V / SNorm[:, None]).astype(np.float64)))
+    L = len(Pts)
+    for it in range(niters):
+        nxt = list(Pts) if it == 0 else Pts
+        for i in range(L):
+            nxt[i] = snf_step(Pts, i, JV[i][0], JV[i][1], reg_diag)
+        Pts = nxt
+    return _fused_sum(Pts)
+
+
+def _fused_sum(Pts):
+    F = np.zeros(Pts[0].shape)
+    for P in Pts:
+        F += P
+    return F / len(Pts)

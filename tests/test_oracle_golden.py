@@ -139,3 +139,10 @@ def test_simple_features_unit_columns():
     F = npo.simple_features(X)
     assert F.shape == (12, 20)
     np.testing.assert_allclose(np.linalg.norm(F, axis=0), 1.0, rtol=1e-12)
+
+
+def test_np_snf_fused(gold):
+    """The SNF step restatement (np_oracle.snf_step, the checker of acoss_snf_step), iterated with
+    the reference's list aliasing, reproduces the reference's doSimilarityFusion output bit for bit."""
+    fused = npo.snf_fused(list(gold["snf_D"]), K=5, niters=5, reg_diag=1)
+    np.testing.assert_array_equal(fused, gold["snf_fused"])  # bit-exact
