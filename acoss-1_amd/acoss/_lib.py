@@ -123,6 +123,20 @@ def _check_pairs(pairs, n_tracks):
         raise ValueError("pair indices must lie in [0, %d)" % n_tracks)
 
 
+def _check_knn(J, n):
+    """Host-side check of kNN column indices (n, K) before a kernel gathers the rows they name:
+    every entry in [0, n), no repeated column within a row (scipy's coo -> csr would merge a
+    repeat into one term, so the product would differ from the reference)."""
+    if J.numel() == 0:
+        return
+    if int(J.min()) < 0 or int(J.max()) >= n:
+        raise ValueError("kNN column indices must lie in [0, %d)" % n)
+    if J.shape[1] > 1:
+        Js = J.sort(dim=1).values
+        if bool((Js[:, 1:] == Js[:, :-1]).any()):
+            raise ValueError("kNN column indices repeat within a row")
+
+
 def crp_params(m=9, tau=1, kappa=0.095, oti=True, gamma_open=0.5, gamma_ext=0.5):
     return CrpParams(int(m), int(tau), float(kappa), int(bool(oti)), float(gamma_open), float(gamma_ext))
 
@@ -307,10 +321,13 @@ def snf_step(mats, skip, J, V, reg_diag, out=None):
     for m in mats:
         if m.dtype != torch.float64 or not m.is_cuda or tuple(m.shape) != (n, n) or not m.is_contiguous():
             raise ValueError("snf_step: every matrix must be a contiguous (n, n) float64 device tensor")
+    if len(mats) < 2:
+        raise ValueError("snf_step: needs at least two matrices (the step averages the others)")
     Jd = _dev(J, torch.int32).contiguous()
     Vd = _dev(V, torch.float64).contiguous()
     if Jd.shape != Vd.shape or Jd.dim() != 2 or Jd.shape[0] != n:
         raise ValueError("snf_step: J and V must both be (n, K)")
+    _check_knn(Jd, n)
     if out is None:
         out = torch.empty((n, n), dtype=torch.float64, device=mats[0].device)
     ptrs = (ctypes.c_void_p * len(mats))(*[m.data_ptr() for m in mats])

@@ -40,7 +40,8 @@ def _getW(D, K, Mu=0.5):
     DSym = 0.5 * (D + D.T)
     DSym.fill_diagonal_(0)
     Neighbs = torch.topk(DSym, K + 1, dim=1, largest=False).values
-    MeanDist = Neighbs.mean(1) * (float(K + 1) / float(K))
+    # the reference's order: (mean * (K + 1)) / K, in the input dtype (similarity_fusion.py:27)
+    MeanDist = Neighbs.mean(1) * float(K + 1) / float(K)
     Eps = (MeanDist[:, None] + MeanDist[None, :] + DSym) / 3
     Denom = 2 * (Mu * Eps) ** 2
     Denom[Denom == 0] = 1
@@ -134,7 +135,15 @@ def _fusion_ws(Ws, K=5, niters=20, reg_diag=1):
     Pts = [P.to(torch.float64).contiguous() for P in Ps]
     N = len(Pts)
     if N < 2:
-        raise ValueError("doSimilarityFusionWs needs at least two matrices")
+        if N == 0:
+            raise IndexError("list index out of range")  # the reference's Ws[0] (similarity_fusion.py:167)
+        if niters > 0:
+            # the reference divides the empty sum by float(N - 1) = 0 (similarity_fusion.py:176):
+            # 0/0 = nan everywhere, which every later step keeps
+            import warnings
+            warnings.warn("invalid value encountered in divide", RuntimeWarning, stacklevel=3)
+            return torch.full(Pts[0].shape, float("nan"), dtype=torch.float64, device=Pts[0].device)
+        return Pts[0].clone()
     for it in range(niters):
         # the reference's `Pts = nextPts` aliasing: from the second iteration on, matrix i's
         # update already sees the new matrices k < i; replacing Pts[i] in place of the list

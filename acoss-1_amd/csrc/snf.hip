@@ -23,17 +23,21 @@
 namespace acoss {
 namespace {
 
-constexpr int kSnfMaxMats = 8;
+// The matrices to average reach the kernel as kernel-argument chunks of kSnfChunk pointers;
+// more than one chunk is summed in passes through a scratch matrix (same summation order).
+constexpr int kSnfChunk = 16;
 constexpr int kSnfMaxK = 64;
 
 struct MatPtrs {
-  const double* p[kSnfMaxMats];
+  const double* p[kSnfChunk];
 };
 
-// Per row: the K (column, value) pairs sorted by column (insertion sort; K <= 64, rows
-// have no repeated columns), so both products sum in csr order.
+// Per row: the K (column, value) pairs sorted by column (insertion sort; K <= 64), so both
+// products sum in csr order. A row whose columns leave [0, n) or repeat (scipy's coo -> csr
+// would merge repeats into one term) raises *err and is replaced by one harmless entry
+// (its own column, weight 0), so no later kernel reads outside the matrices.
 __global__ void k_snf_sort_knn(const int32_t* __restrict__ J, const double* __restrict__ V, int32_t n, int32_t K,
-                               int32_t* __restrict__ Js, double* __restrict__ Vs) {
+                               int32_t* __restrict__ Js, double* __restrict__ Vs, int32_t* __restrict__ err) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   int32_t jj[kSnfMaxK];
@@ -50,6 +54,15 @@ __global__ void k_snf_sort_knn(const int32_t* __restrict__ J, const double* __re
     jj[q] = c;
     vv[q] = v;
   }
+  bool ok = jj[0] >= 0 && jj[K - 1] < n;
+  for (int k = 1; k < K; ++k) ok = ok && jj[k] != jj[k - 1];
+  if (!ok) {
+    *err = 1;
+    for (int k = 0; k < K; ++k) {
+      jj[k] = r;
+      vv[k] = 0.0;
+    }
+  }
   for (int k = 0; k < K; ++k) {
     Js[(int64_t)r * K + k] = jj[k];
     Vs[(int64_t)r * K + k] = vv[k];
@@ -57,12 +70,15 @@ __global__ void k_snf_sort_knn(const int32_t* __restrict__ J, const double* __re
 }
 
 // At[c, a] = (sum_{m != skip} mats[m][a, c]) / (n_mats - 1): 64 x 64 tile through LDS.
-__global__ __launch_bounds__(256) void k_snf_avg_t(MatPtrs mats, int32_t n_mats, int32_t skip, int32_t n,
+// One launch sums a chunk of `cnt` matrices (the skipped one already left out, ascending m)
+// onto the running sum `part` (untransposed; NULL for the first chunk). A chunk that is not
+// the last writes the running sum to `part_out` untransposed; the last divides and writes At.
+__global__ __launch_bounds__(256) void k_snf_avg_t(MatPtrs mats, int32_t cnt, int32_t n, double denom,
+                                                   const double* __restrict__ part, double* __restrict__ part_out,
                                                    double* __restrict__ At) {
   __shared__ double tile[64][65];
   const int a0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   const int t = threadIdx.x;
-  const double denom = (double)(n_mats - 1);
 #pragma unroll 4
   for (int r = 0; r < 16; ++r) {
     const int idx = t + 256 * r;
@@ -70,14 +86,16 @@ __global__ __launch_bounds__(256) void k_snf_avg_t(MatPtrs mats, int32_t n_mats,
     double s = 0.0;
     if (a < n && c < n) {
       const int64_t e = (int64_t)a * n + c;
-      for (int m = 0; m < n_mats; ++m) {
-        if (m == skip) continue;
-        s = s + mats.p[m][e];
-      }
-      s = s / denom;
+      if (part) s = part[e];
+      for (int m = 0; m < cnt; ++m) s = s + mats.p[m][e];
+      if (part_out)
+        part_out[e] = s;
+      else
+        s = s / denom;
     }
     tile[idx & 63][idx >> 6] = s;
   }
+  if (part_out) return;  // uniform per launch
   __syncthreads();
 #pragma unroll 4
   for (int r = 0; r < 16; ++r) {
@@ -171,18 +189,17 @@ extern "C" int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t
                               const int32_t* J, const double* V, int32_t K, double reg_diag, double* out,
                               void* hip_stream) {
   clear_error();
-  if (!mats || n_mats < 2 || n_mats > kSnfMaxMats || skip < 0 || skip >= n_mats || n <= 0 || !J || !V || !out ||
-      K <= 0 || K > kSnfMaxK || K > n) {
-    set_error("acoss_snf_step: bad arguments (need 2 <= n_mats <= %d, 0 < K <= min(n, %d))", kSnfMaxMats, kSnfMaxK);
+  if (!mats || n_mats < 2 || skip < 0 || skip >= n_mats || n <= 0 || !J || !V || !out || K <= 0 ||
+      K > kSnfMaxK || K > n) {
+    set_error("acoss_snf_step: bad arguments (need n_mats >= 2, 0 <= skip < n_mats, 0 < K <= min(n, %d))",
+              kSnfMaxK);
     return ACOSS_E_ARG;
   }
-  MatPtrs mp{};
   for (int m = 0; m < n_mats; ++m) {
     if (!mats[m] || (m != skip && mats[m] == out)) {
       set_error("acoss_snf_step: matrix %d is NULL or aliases the output", m);
       return ACOSS_E_ARG;
     }
-    mp.p[m] = mats[m];
   }
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   const size_t nn = (size_t)n * n;
@@ -193,11 +210,38 @@ extern "C" int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t
   double* At = reinterpret_cast<double*>(ws + nn * 8);
   double* Vs = reinterpret_cast<double*>(ws + 2 * nn * 8);
   int32_t* Js = reinterpret_cast<int32_t*>(ws + 2 * nn * 8 + knn * 8);
+  int32_t* d_err = reinterpret_cast<int32_t*>(ws + 2 * nn * 8 + knn * 12);
   const unsigned nt = (unsigned)((n + 63) / 64);
-  hipLaunchKernelGGL(k_snf_sort_knn, dim3((n + 255) / 256), dim3(256), 0, s, J, V, n, K, Js, Vs);
+  ACOSS_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
+  hipLaunchKernelGGL(k_snf_sort_knn, dim3((n + 255) / 256), dim3(256), 0, s, J, V, n, K, Js, Vs, d_err);
   ACOSS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_snf_avg_t, dim3(nt, nt), dim3(256), 0, s, mp, n_mats, skip, n, At);
-  ACOSS_LAUNCH_CHECK();
+  // the kNN columns are checked before any product reads a row they name
+  int h_err = 0;
+  ACOSS_HIP_CHECK(hipMemcpyAsync(&h_err, d_err, 4, hipMemcpyDeviceToHost, s));
+  ACOSS_HIP_CHECK(hipStreamSynchronize(s));
+  if (h_err) {
+    set_error("acoss_snf_step: kNN column indices must lie in [0, %d) without repeats within a row", n);
+    return ACOSS_E_ARG;
+  }
+  // average of the other matrices, ascending m, in chunks of kSnfChunk pointers; the running
+  // sum of a multi-chunk average lives in Bm (free until the first product)
+  const double denom = (double)(n_mats - 1);
+  MatPtrs mp{};
+  int cnt = 0, done = 0;
+  const double* part = nullptr;
+  for (int m = 0; m < n_mats; ++m) {
+    if (m == skip) continue;
+    mp.p[cnt++] = mats[m];
+    ++done;
+    if (cnt == kSnfChunk || done == n_mats - 1) {
+      const bool last = done == n_mats - 1;
+      hipLaunchKernelGGL(k_snf_avg_t, dim3(nt, nt), dim3(256), 0, s, mp, cnt, n, denom, part,
+                         last ? nullptr : Bm, At);
+      ACOSS_LAUNCH_CHECK();
+      part = Bm;
+      cnt = 0;
+    }
+  }
   hipLaunchKernelGGL(k_snf_gather_t, dim3(nt, (n + kGJ - 1) / kGJ), dim3(256), 0, s, At, n, K, Js, Vs, Bm);
   ACOSS_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_snf_left, dim3((n + 1023) / 1024, n), dim3(256), 0, s, Bm, n, K, Js, Vs, reg_diag, out);

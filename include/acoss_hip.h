@@ -122,8 +122,12 @@ int acoss_wcsm(const float* CSM, int32_t M, int32_t N, int32_t k1, int32_t k2, f
  *   out = S . A . S^T + reg_diag * I,  A = (sum_{m != skip} mats[m]) / (n_mats - 1),
  * S the kNN-truncated row-normalised affinity (getS, :121-143) given as J (n x K) int32 column
  * indices and V (n x K) float64 values, any order within a row (sums run in ascending column
- * order, as scipy's csr product). mats: HOST array of n_mats device pointers to (n x n) float64
- * matrices; out (n x n) float64 may alias mats[skip] but no other. 2 <= n_mats <= 8, K <= 64. */
+ * order, as scipy's csr product). Every J entry must lie in [0, n) and no column may repeat
+ * within a row (scipy's coo -> csr would merge repeats into one term): otherwise ACOSS_E_ARG,
+ * checked on the device before any product runs. mats: HOST array of n_mats device pointers
+ * to (n x n) float64 matrices; out (n x n) float64 may alias mats[skip] but no other.
+ * n_mats >= 2 (any number; more than 16 others are averaged in passes), 0 < K <= min(n, 64).
+ * Synchronises the stream once (the index check). */
 int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t skip, int32_t n, const int32_t* J,
                    const double* V, int32_t K, double reg_diag, double* out, void* hip_stream);
 

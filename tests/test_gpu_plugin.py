@@ -92,6 +92,19 @@ def test_benchmark_serra09_matches_oracle(tmp_path, monkeypatch):
     assert algo.getEvalStatistics("main")[3] == ref_stats[3]
 
 
+# SNF tolerance on float32 inputs: W, P and S come out of float32 reductions (kNN mean, row
+# sums, kNN weight sums) whose summation order differs from numpy's partition/pairwise order,
+# so they differ from the reference by a few float32 ulps; 20 diffusion steps in float64 keep
+# that at the 1e-6 relative level. The bar below is 1e-5 relative (plus 1e-9 absolute).
+SNF_F32_RTOL = 1e-5
+SNF_F32_ATOL = 1e-9
+
+
+def _assert_snf_close(got, ref):
+    assert got.shape == ref.shape and got.dtype == np.float64
+    np.testing.assert_allclose(got, ref, rtol=SNF_F32_RTOL, atol=SNF_F32_ATOL)
+
+
 def test_benchmark_chen_matches_oracle(tmp_path, monkeypatch):
     from acoss.algorithms.latefusion_chen import ChenFusion
     monkeypatch.chdir(tmp_path)
@@ -105,13 +118,16 @@ def test_benchmark_chen_matches_oracle(tmp_path, monkeypatch):
         a.normalize_by_length()
         norm = np.sqrt(lens.astype(np.float64))[None, :]
         np.testing.assert_array_equal(np.asarray(a.Ds["qmax"]), (norm / Q).astype(np.float32))
-    # late fusion needs finite inputs: replace the inf diagonal as a user of the fused output would see it
-    for k in a.Ds:
-        M = np.asarray(a.Ds[k])
-        M[~np.isfinite(M)] = 1e6
-        a.Ds[k][:] = M
+    # late fusion on the normalised float32 matrices exactly as the reference leaves them,
+    # inf diagonal included (getW's fill_diagonal removes it), vs the numpy restatement
+    # (bit-exact vs the reference's golden doSimilarityFusion in float64)
+    ins = [np.array(a.Ds[k]) for k in a.Ds]
+    assert all(np.isinf(np.diag(m)).all() for m in ins)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ref = npo.snf_fused(ins, K=20, niters=20, reg_diag=1)
     a.do_late_fusion()
-    assert np.all(np.isfinite(a.Ds["Late"]))
+    _assert_snf_close(np.asarray(a.Ds["Late"]), ref)
+    np.testing.assert_array_equal(np.asarray(a.Ds["qmax"]), -ins[0])
 
 
 def test_benchmark_simple_matches_oracle(tmp_path, monkeypatch):
@@ -156,8 +172,12 @@ def test_earlyfusion_composition(tmp_path, monkeypatch):
             for s, key in enumerate(["mfccs", "ssms", "chromas", "early"]):
                 ref = oracle.sw_constrained(mats[s])
                 assert ef.Ds[key][i, j] == np.float32(ref), (i, j, key)  # Ds is float32, like the memmap
+    ins = {s: np.array(ef.Ds[s]) for s in ["chromas", "ssms", "mfccs", "early"]}
     ef.do_late_fusion()
-    assert np.all(np.isfinite(ef.Ds["late"])) and np.all(np.isfinite(ef.Ds["early+late"]))
+    ref_late = npo.snf_fused([1.0 / (1.0 + ins[s]) for s in ["chromas", "ssms", "mfccs"]], K=20, niters=20)
+    ref_el = npo.snf_fused([1.0 / (1.0 + ins[s]) for s in ["chromas", "ssms", "mfccs", "early"]], K=20, niters=20)
+    _assert_snf_close(np.asarray(ef.Ds["late"]), ref_late)
+    _assert_snf_close(np.asarray(ef.Ds["early+late"]), ref_el)
 
 
 @pytest.mark.parametrize("n,K,L", [(40, 5, 2), (333, 20, 3), (1030, 7, 4)])
@@ -178,12 +198,79 @@ def test_snf_step_bitexact(n, K, L):
     np.testing.assert_array_equal(got, npo.snf_step(mats, 0, J, V, 0.0))
 
 
+def test_snf_step_many_matrices():
+    """More matrices than one kernel-argument chunk (16): the average runs in passes and stays
+    bit-exact (same ascending summation order)."""
+    import torch
+    n, K, L = 70, 6, 37
+    rng = np.random.default_rng(7)
+    mats = [rng.random((n, n)) for _ in range(L)]
+    J = np.stack([rng.choice(n, K, replace=False) for _ in range(n)]).astype(np.int32)
+    V = rng.random((n, K))
+    dm = [torch.as_tensor(m).cuda() for m in mats]
+    for skip in (0, 16, 17, L - 1):
+        got = _lib.snf_step(dm, skip, J, V, 1.0).cpu().numpy()
+        np.testing.assert_array_equal(got, npo.snf_step(mats, skip, J, V, 1.0))
+
+
+def test_snf_float32_matches_restatement():
+    """doSimilarityFusion on float32 distance matrices (the ChenFusion / EarlyFusion input dtype)
+    vs the numpy restatement at the stated SNF tolerance, with an inf diagonal as Chen has."""
+    from acoss.algorithms.utils.similarity_fusion import doSimilarityFusion
+    rng = np.random.default_rng(5)
+    n = 150
+    Ds = []
+    for _ in range(3):
+        D = (rng.random((n, n)) * 10 + 0.5).astype(np.float32)
+        np.fill_diagonal(D, np.inf)
+        Ds.append(D)
+    Ws, fused = doSimilarityFusion(Ds, K=20, niters=20, reg_diag=1)
+    with np.errstate(invalid="ignore"):
+        ref = npo.snf_fused(Ds, K=20, niters=20, reg_diag=1)
+    assert Ws[0].dtype == np.float32
+    _assert_snf_close(fused, ref)
+
+
+def test_snf_single_matrix_is_nan():
+    """One matrix: the reference divides the empty average by N - 1 = 0, so every entry is nan."""
+    from acoss.algorithms.utils.similarity_fusion import doSimilarityFusionWs
+    W = np.random.default_rng(1).random((12, 12))
+    with pytest.warns(RuntimeWarning):
+        F = doSimilarityFusionWs([W], K=3, niters=2)
+    assert F.shape == (12, 12) and np.isnan(F).all()
+
+
 def test_snf_step_rejects_bad_args():
+    import ctypes
     import torch
     m = torch.zeros((8, 8), dtype=torch.float64, device="cuda")
-    J = np.zeros((8, 2), np.int32)
+    J = np.tile(np.arange(2, dtype=np.int32), (8, 1))
     V = np.zeros((8, 2))
-    with pytest.raises(_lib.AcossHipError):
+    with pytest.raises(ValueError):
         _lib.snf_step([m], 0, J, V, 1.0)  # one matrix: nothing to average
     with pytest.raises(ValueError):
         _lib.snf_step([m, m.float()], 0, J, V, 1.0)
+    for bad in (8, -1):  # column outside [0, n)
+        Jb = J.copy()
+        Jb[3, 1] = bad
+        with pytest.raises(ValueError):
+            _lib.snf_step([m, m.clone()], 0, Jb, V, 1.0)
+    Jd = J.copy()
+    Jd[5] = [4, 4]  # repeated column in a row
+    with pytest.raises(ValueError):
+        _lib.snf_step([m, m.clone()], 0, Jd, V, 1.0)
+    # the C-ABI checks the same on the device (a caller that skips the Python wrapper)
+    lib = _lib.load_library()
+    m2 = m.clone()
+    out = torch.empty_like(m)
+    ptrs = (ctypes.c_void_p * 2)(m.data_ptr(), m2.data_ptr())
+    Vd = torch.as_tensor(V).cuda()
+    for Jbad in (Jb, Jd, np.full((8, 2), 1 << 20, np.int32)):
+        Jt = torch.as_tensor(Jbad).cuda()
+        rc = lib.acoss_snf_step(ptrs, 2, 0, 8, ctypes.c_void_p(Jt.data_ptr()), ctypes.c_void_p(Vd.data_ptr()), 2,
+                                1.0, ctypes.c_void_p(out.data_ptr()), _lib._stream())
+        assert rc == -1 and b"kNN column" in lib.acoss_last_error()
+    Jt = torch.as_tensor(J).cuda()
+    rc = lib.acoss_snf_step(ptrs, 2, 0, 8, ctypes.c_void_p(Jt.data_ptr()), ctypes.c_void_p(Vd.data_ptr()), 2, 1.0,
+                            ctypes.c_void_p(out.data_ptr()), _lib._stream())
+    assert rc == 0
