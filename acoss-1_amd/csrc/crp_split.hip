@@ -30,7 +30,7 @@ namespace {
 constexpr int kMS = 9;
 
 #ifdef ACOSS_STAMPS  // diagnostic builds only: per-phase cycle sums of the fused sweep
-__device__ unsigned long long d_sweep_stamps[16];
+__device__ unsigned long long d_sweep_stamps[32];
 __device__ __forceinline__ unsigned long long sstamp() {
   unsigned long long t;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -156,6 +156,10 @@ struct LineCells {
 
 constexpr int kTP = 34;  // tile pitch in halfwords: 17 words, odd -> lane stride hits distinct banks
 
+// Position of strip row r in a column's 32-row run of the strip-major plane: SPLIT word order
+// (word h = rows h and h + 16, see Line), so the column select loads its words ready to use.
+__device__ __forceinline__ constexpr int spos(int r) { return (r & 15) * 2 + (r >> 4); }
+
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 // Global-address-space u16 pointer: a pointer pinned to SGPRs by an empty asm loses its address
 // space, and generic (flat) stores count in lgkmcnt too, so every s_waitcnt for the LDS reads
@@ -164,6 +168,9 @@ typedef __attribute__((address_space(1))) uint16_t gu16;
 // Store at a 32-bit byte offset from an SGPR base: global_store_short v_off, v, s[base] (saddr
 // form; a u16 element index would need a 64-bit address per store).
 __device__ __forceinline__ void st_u16(gu16* base, unsigned idx, unsigned v) {
+#ifdef ACOSS_ABL_NOHR  // timing ablation only (wrong results): no row-major plane stores
+  return;
+#endif
   typedef __attribute__((address_space(1))) char gchar;
   *(gu16*)((gchar*)base + idx * 2u) = (uint16_t)v;
 }
@@ -214,7 +221,7 @@ __device__ __forceinline__ void diag_pk(const PairView& V, int i0, int td, int j
     const unsigned key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
     const int col = j0 + td + r;
     st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), key >> 16);  // pad column for out-of-range
-    tileT[(td + r) * kTP + r] = (uint16_t)(key >> 16);
+    tileT[(td + r) * kTP + spos(r)] = (uint16_t)(key >> 16);
   };
   auto emit2 = [&](int r, f32x2 dot, gu16* hrow) {  // rows r, r + 1 (cells on this diagonal)
     const f32x2 nq = f32x2{nqr(r), nqr(r + 1)};
@@ -225,8 +232,8 @@ __device__ __forceinline__ void diag_pk(const PairView& V, int i0, int td, int j
     const int col = j0 + td + r;
     st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), k0 >> 16);
     st_u16(hrow, ldr + min((unsigned)(col + 1), (unsigned)(ldr - 1)), k1 >> 16);
-    tileT[(td + r) * kTP + r] = (uint16_t)(k0 >> 16);
-    tileT[(td + r + 1) * kTP + r + 1] = (uint16_t)(k1 >> 16);
+    tileT[(td + r) * kTP + spos(r)] = (uint16_t)(k0 >> 16);
+    tileT[(td + r + 1) * kTP + spos(r + 1)] = (uint16_t)(k1 >> 16);
   };
   auto window1 = [&](int r) {
     float dot = G[r];
@@ -450,7 +457,7 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
         if (FAST || r < rows) st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), key >> 16);
         hrow += ldr;  // next row: one scalar add instead of 32 hoisted row pointers
         asm volatile("" : "+s"(hrow));
-        tileT[(t + r) * kTP + r] = (uint16_t)(key >> 16);
+        tileT[(t + r) * kTP + spos(r)] = (uint16_t)(key >> 16);
       }
     }
     }  // !FAST
@@ -459,7 +466,11 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
     ACOSS_STAMP(t3);
     // columns [j0, j0 + 256) complete: column-major prefixes, 32 rows = 64 B per column
     const int jj = j0 + t;
+#ifdef ACOSS_ABL_NOHC  // timing ablation only (wrong results): no strip-major plane stores
+    if (false) {
+#else
     if (jj >= 0 && jj < V.Np) {
+#endif
       const uint32_t* src = reinterpret_cast<const uint32_t*>(tileT + t * kTP);
       uint4* dh = reinterpret_cast<uint4*>(Hc + ((size_t)strip * ldc + jj) * kSR);  // [strip][column][32 rows]
 #pragma unroll
@@ -523,12 +534,24 @@ __device__ __forceinline__ unsigned pk_add_u16(unsigned a, unsigned b) {
   return __builtin_bit_cast(unsigned, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
 }
 
+// Bits h and h + 16 of the result take the per-field flags (bits 15 and 31) of SWAR word h.
+__device__ __forceinline__ uint32_t gather_flags(uint32_t acc, uint32_t s, int h) {
+  return ((s >> (15 - h)) & (0x00010001u << h)) | acc;
+}
+
+// Lane l holds its KPL = 32 elements (element q = line element 32 l + q) as 16 packed words in
+// SPLIT order: word h = element h (bits 0..15) and element h + 16 (bits 16..31). In this order
+// the flag bits of a SWAR compare on word h (bits 15 and 31) become mask bits h and h + 16 with
+// one shift and one and-or, so an element mask costs 3 VALU per word.
 template <int KPL>
 struct Line {
+  static_assert(KPL == 32, "split word order assumes 32 elements per lane");
   unsigned pv[KPL / 2];
-  __device__ __forceinline__ unsigned pfx(int q) const { return (q & 1) ? (pv[q >> 1] >> 16) : (pv[q >> 1] & 0xffffu); }
-  // lane l's KPL elements start at col0 + l * lane_stride (strip-major column plane): the
-  // loaded words already are the packed pairs
+  __device__ __forceinline__ unsigned pfx(int q) const { return q < 16 ? (pv[q] & 0xffffu) : (pv[q - 16] >> 16); }
+  // Lane l's KPL elements start at col0 + l * lane_stride. STORED_SPLIT: the plane holds every
+  // run in split order already (the strip-major column plane, written so by the sweep);
+  // otherwise (row-major plane, natural order) the loaded pairs are repacked, one v_perm per word.
+  template <bool STORED_SPLIT>
   __device__ __forceinline__ void load_lanes(const uint16_t* col0, size_t lane_stride, int n) {
     const int lane = threadIdx.x & 63;
     const int base = lane * KPL;
@@ -538,29 +561,33 @@ struct Line {
     // conditional loads: hipcc branches around each and waits vmcnt(0) after each (16-32
     // serial L2 round trips per line)
     const uint16_t* src = col0 + (base < n ? (size_t)lane * lane_stride : (size_t)0);
+    unsigned w[KPL / 2];
 #pragma unroll
     for (int q = 0; q < KPL / 8; ++q) {
-      const uint4 w = reinterpret_cast<const uint4*>(src)[q];
-      pv[4 * q + 0] = w.x;
-      pv[4 * q + 1] = w.y;
-      pv[4 * q + 2] = w.z;
-      pv[4 * q + 3] = w.w;
+      const uint4 v = reinterpret_cast<const uint4*>(src)[q];
+      w[4 * q + 0] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+    if (STORED_SPLIT) {
+#pragma unroll
+      for (int h = 0; h < KPL / 2; ++h) pv[h] = w[h];
+    } else {
+#pragma unroll
+      for (int h = 0; h < KPL / 2; ++h)  // (element h, element h + 16) from natural pairs
+        pv[h] = __builtin_amdgcn_perm(w[8 + (h >> 1)], w[h >> 1], (h & 1) ? 0x07060302u : 0x05040100u);
     }
     if (base + KPL > n) {
       int nv = n - base;  // opaque per call: no hoisted per-element predicates in callers' loops
       asm volatile("" : "+v"(nv));
 #pragma unroll
       for (int h = 0; h < KPL / 2; ++h) {
-        const unsigned a = (2 * h < nv) ? (pv[h] & 0xffffu) : kNone;
-        const unsigned b = (2 * h + 1 < nv) ? (pv[h] >> 16) : kNone;
+        const unsigned a = (h < nv) ? (pv[h] & 0xffffu) : kNone;
+        const unsigned b = (h + 16 < nv) ? (pv[h] >> 16) : kNone;
         pv[h] = a | (b << 16);
       }
     }
-  }
-  // from full keys (0xffffffff = none): high halves of two keys in one v_perm, clamped to kNone
-  __device__ __forceinline__ void from_full(const unsigned* f) {
-#pragma unroll
-    for (int h = 0; h < KPL / 2; ++h) pv[h] = pk_min_u16(__builtin_amdgcn_perm(f[2 * h + 1], f[2 * h], 0x07060302u), 0x7fff7fffu);
   }
   // #elements <= x (x <= 0x7fff): per field (x + 0x8000) - a keeps bit 15 iff a <= x, with no
   // borrow across fields; popcount on VALU, one DPP wave sum (no SGPR per compare, no SALU).
@@ -579,26 +606,20 @@ struct Line {
 #endif
   }
   // Bit q set iff element q's prefix == P (P <= 0x7f80). Per field, (a ^ P) + 0x7fff keeps bit
-  // 15 iff a != P; fields are <= 0x7fff, so nothing carries across. Elements past KPL: 0.
+  // 15 iff a != P; fields are <= 0x7fff, so nothing carries across.
   __device__ __forceinline__ uint32_t eq_mask(unsigned P) const {
     const unsigned PP = P * 0x10001u;
     uint32_t ne = 0;
 #pragma unroll
-    for (int h = 0; h < KPL / 2; ++h) {
-      const unsigned s = (pv[h] ^ PP) + 0x7fff7fffu;
-      ne |= (((s >> 15) & 1u) << (2 * h)) | ((s >> 31) << (2 * h + 1));
-    }
-    return KPL >= 32 ? ~ne : ~ne & ((1u << KPL) - 1u);
+    for (int h = 0; h < KPL / 2; ++h) ne = gather_flags(ne, (pv[h] ^ PP) + 0x7fff7fffu, h);
+    return ~ne;
   }
   // Bit q set iff element q's prefix <= x (x <= 0x7fff; kNone is never <= a real x).
   __device__ __forceinline__ uint32_t le_mask(unsigned x) const {
     const unsigned X2 = (x + 0x8000u) * 0x10001u;
     uint32_t le = 0;
 #pragma unroll
-    for (int h = 0; h < KPL / 2; ++h) {
-      const unsigned s = X2 - pv[h];
-      le |= (((s >> 15) & 1u) << (2 * h)) | ((s >> 31) << (2 * h + 1));
-    }
+    for (int h = 0; h < KPL / 2; ++h) le = gather_flags(le, X2 - pv[h], h);
     return le;
   }
   // min over elements (kNone is above every real prefix) and max over real elements
@@ -674,6 +695,13 @@ __device__ __forceinline__ unsigned prefix_of_rank(const Line<KPL>& L, int rho, 
   *less_out = c_am1;
   return a;
 }
+
+// Search state carried from one line to the next of a wave's run: the previous line's answer
+// prefix and the local density (elements per prefix unit) seen around it.
+struct Hint {
+  unsigned P;  // kNoHint: none
+  float dens;
+};
 
 // Scratch of one wave in LDS: element list and 64 bit-words.
 struct WaveLds {
@@ -860,18 +888,32 @@ __device__ unsigned rank_in_prefix(const Line<KPL>& L, unsigned P, int rho, int 
 // exact keys of the last batched group in *cache for le_bits.
 template <int KPL, class KF>
 __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF& keyf, WaveLds& W, Group* c_lo,
-                               Group* c_hi, float* thr, float* T, unsigned* hint) {
+                               Group* c_hi, float* thr, float* T, Hint* hint) {
   const float q = (float)(n - 1) * kappa;
   const float lo_f = floorf(q), hi_f = ceilf(q);
   const int lo = (int)lo_f, hi = (int)hi_f;
   unsigned kmin = 0, kmax = 0x7f80u;  // every real prefix (finite non-negative float) is <= 0x7f80
-  if (*hint == kNoHint) L.min_max(&kmin, &kmax);
+  const bool hinted = hint->P != kNoHint;
+  if (!hinted) L.min_max(&kmin, &kmax);
   int le, less;
   int passes = 0;
-  const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, *hint, &le, &less, &passes);
+  const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, hint->P, &le, &less, &passes);
   ACOSS_COUNT(KF::kRow ? 6 : 11, 1);
   ACOSS_COUNT(KF::kRow ? 7 : 12, passes);
-  *hint = Pl;
+  if (!hinted) {
+    ACOSS_COUNT(KF::kRow ? 16 : 18, 1);
+    ACOSS_COUNT(KF::kRow ? 17 : 19, passes);
+  }
+#ifdef ACOSS_STAMPS
+  if (hinted) {
+    const unsigned dlt = Pl > hint->P ? Pl - hint->P : hint->P - Pl;
+    const int bin = dlt == 0 ? 0 : dlt == 1 ? 1 : dlt == 2 ? 2 : dlt <= 4 ? 3 : dlt <= 8 ? 4 : dlt <= 16 ? 5 : dlt <= 32 ? 6 : 7;
+    ACOSS_COUNT(20 + bin, 1);
+  }
+#endif
+  hint->P = Pl;
+  // density around the answer: the group at Pl, smoothed over the run
+  hint->dens = hinted ? 0.5f * hint->dens + 0.5f * (float)(le - less) : (float)(le - less);
   unsigned vlo, vhi;
 #ifdef ACOSS_ABL_NOGROUP
   if (true) {
@@ -907,42 +949,40 @@ __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF&
   *T = sq_threshold(th);
 }
 
-// Bits of "key <= T" for the KPL elements of this lane (element e = lane*KPL + q). Decided on
-// the prefix; the elements whose prefix equals T's are decided on exact keys from a batched
-// group (reused from the threshold search when it has that prefix).
+// Bits of "key <= T" for the KPL elements of this lane (element e = lane*KPL + q): every
+// element whose prefix is <= T's prefix, minus the members of T's prefix group whose exact key
+// exceeds T. The group's exact keys come from the threshold search (the group at the answer's
+// prefix, cached), so normally no member mask or recompute is needed here.
 template <int KPL, class KF>
 __device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, WaveLds& W, const Group& c_lo,
                             const Group& c_hi) {
   const unsigned T16 = Tbits >> 16;
   const int lane = threadIdx.x & 63;
-  // k < T16 and k == T16 as SWAR masks (kNone is never <= T16 <= 0x7f80)
-  const uint32_t word = T16 ? L.le_mask(T16 - 1) : 0u;
-  const int g = wave_sum(__builtin_popcount(L.eq_mask(T16)));
-  if (g == 0) return word;
-  if (g <= 64) {
-    Group G;
-    if (c_lo.g >= 0 && c_lo.P == T16)
-      G = c_lo;
-    else if (c_hi.g >= 0 && c_hi.P == T16)
-      G = c_hi;
-    else
-    {
+  const uint32_t word = L.le_mask(T16);  // kNone is never <= T16 <= 0x7f80
+  // (selected by value: a pointer to either cached group would put both on the stack)
+  const bool lo_hit = c_lo.g >= 0 && c_lo.P == T16, hi_hit = c_hi.g >= 0 && c_hi.P == T16;
+  W.words[lane] = 0xffffffffu;
+  __builtin_amdgcn_wave_barrier();
+  if (lo_hit || hi_hit) {
+    const int cg = lo_hit ? c_lo.g : c_hi.g;
+    const unsigned ckey = lo_hit ? c_lo.key : c_hi.key;
+    const int celem = lo_hit ? c_lo.elem : c_hi.elem;
+    if (lane < cg && ckey > Tbits) atomicAnd(&W.words[celem / KPL], ~(1u << (celem % KPL)));
+  } else {
+    const int g = wave_sum(__builtin_popcount(L.eq_mask(T16)));
+    if (g == 0) return word;
+    if (g <= 64) {
       ACOSS_COUNT(KF::kRow ? 10 : 15, 1);
-      G = group_keys(L, T16, g, keyf, W);
+      const Group G = group_keys(L, T16, g, keyf, W);
+      if (lane < G.g && G.key > Tbits) atomicAnd(&W.words[G.elem / KPL], ~(1u << (G.elem % KPL)));
+    } else {  // large group: member keys in rounds of 64
+      group_rounds(L, T16, g, W, [&](int e) {
+        if (keyf(e) > Tbits) atomicAnd(&W.words[e / KPL], ~(1u << (e % KPL)));
+      });
     }
-    W.words[lane] = 0u;
-    __builtin_amdgcn_wave_barrier();
-    if (lane < G.g && G.key <= Tbits) atomicOr(&W.words[G.elem / KPL], 1u << (G.elem % KPL));
-    __builtin_amdgcn_wave_barrier();
-    return word | W.words[lane];
   }
-  W.words[lane] = 0u;  // large group: member bits in rounds of 64
   __builtin_amdgcn_wave_barrier();
-  group_rounds(L, T16, g, W, [&](int e) {
-    if (keyf(e) <= Tbits) atomicOr(&W.words[e / KPL], 1u << (e % KPL));
-  });
-  __builtin_amdgcn_wave_barrier();
-  return word | W.words[lane];
+  return word & W.words[lane];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -985,12 +1025,12 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // w: wave-uniform (SGPR)
   WaveLds& W = wl[w];
   constexpr int RPW = kSR / NW;  // consecutive rows per wave: each search starts from its neighbour's
-  unsigned hint = kNoHint;
+  Hint hint{kNoHint, 1.0f};
   // the next row's line is loaded while this one is searched (its latency hidden)
   auto load_row = [&](Line<KPL>& Ld, int i) {
     int64_t rowoff = (int64_t)p * kstride + (int64_t)i * ldr;
     asm volatile("" : "+s"(rowoff));  // per-row address: nothing per lane hoisted out of the loop
-    Ld.load_lanes(K.hr + rowoff, KPL, V.Np);
+    Ld.template load_lanes<false>(K.hr + rowoff, KPL, V.Np);
   };
   Line<KPL> Lnext;
   if (i0 + w * RPW < V.Mp) load_row(Lnext, i0 + w * RPW);
@@ -1117,13 +1157,13 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
   const int j0 = (lb - p * gridDim.x) * kColsPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCPW;
   WaveLds& W = wl[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
-  unsigned hint = kNoHint;
+  Hint hint{kNoHint, 1.0f};
   const int jend = min(j0 + kCPW, V.Np);
   // the next column's line is loaded while this one is searched (its HBM latency hidden)
   auto load_col = [&](Line<KPL>& Ld, int j) {
     int64_t coloff = (int64_t)p * kstride + (int64_t)j * kSR;
     asm volatile("" : "+s"(coloff));  // per-column address: nothing per lane hoisted out of the loop
-    Ld.load_lanes(K.hc + coloff, (size_t)ldc * kSR, V.Mp);
+    Ld.template load_lanes<true>(K.hc + coloff, (size_t)ldc * kSR, V.Mp);
   };
 #ifdef ACOSS_COLS_NOPF  // no next-column prefetch: 16 VGPRs fewer (occupancy over latency)
 #pragma unroll 1
@@ -1206,9 +1246,9 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
 #ifdef ACOSS_STAMPS
 extern "C" int acoss_debug_sweep_stamps(unsigned long long* out16) {
   if (hipDeviceSynchronize() != hipSuccess) return ACOSS_E_HIP;
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(acoss::d_sweep_stamps), 16 * sizeof(unsigned long long)) != hipSuccess)
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(acoss::d_sweep_stamps), 32 * sizeof(unsigned long long)) != hipSuccess)
     return ACOSS_E_HIP;
-  unsigned long long z[16] = {};
+  unsigned long long z[32] = {};
   if (hipMemcpyToSymbol(HIP_SYMBOL(acoss::d_sweep_stamps), z, sizeof(z)) != hipSuccess) return ACOSS_E_HIP;
   return ACOSS_OK;
 }

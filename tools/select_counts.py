@@ -22,7 +22,7 @@ T = len(tracks)
 allp = np.array([(i, j) for i in range(T) for j in range(i + 1, T)], np.int32)
 sel = np.random.default_rng(0).choice(len(allp), 2000, replace=False)
 pairs = torch.as_tensor(allp[np.sort(sel)]).cuda()
-out = (ctypes.c_ulonglong * 16)()
+out = (ctypes.c_ulonglong * 32)()
 lib.acoss_debug_sweep_stamps(out)
 bank.crp_align(pairs)
 torch.cuda.synchronize()
@@ -31,3 +31,8 @@ for name, b in (("rows", 6), ("cols", 11)):
     n = max(out[b], 1)
     print("%s: lines %d  passes/line %.2f  group recomputes/line %.3f  mean group %.2f  le_bits recomputes/line %.3f"
           % (name, out[b], out[b + 1] / n, out[b + 2] / n, out[b + 3] / max(out[b + 2], 1), out[b + 4] / n))
+for name, b in (("rows", 16), ("cols", 18)):
+    n = max(out[b], 1)
+    print("%s unhinted: lines %d  passes/line %.2f" % (name, out[b], out[b + 1] / n))
+h = [out[20 + k] for k in range(8)]
+print("|P - hint| histogram (0,1,2,3-4,5-8,9-16,17-32,>32):", h, ["%.3f" % (x / max(sum(h), 1)) for x in h])
