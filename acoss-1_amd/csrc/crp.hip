@@ -1071,7 +1071,9 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   // split path (one sweep + two line-select kernels, crp_split.hip) needs 16-bit key planes
   static const char* path_env = getenv("ACOSS_CRP_PATH");
   const bool split = m == 9 && L <= 2048 && !(path_env && strcmp(path_env, "fused") == 0);
-  const int ldk = (int)align_up((size_t)L + 1, 64);  // >= 1 pad column (sweep's branchless stores)
+  // row pitch: the selects' 32-element runs end at align32(L); one pad column beyond them takes
+  // the sweep's branchless out-of-range stores
+  const int ldk = (int)align_up(align_up((size_t)L, 32) + 1, 64);
   const int64_t kstride = split ? (int64_t)align_up((size_t)L, 32) * ldk : 0;  // whole 32-row strips
   // Two-level batching: a DP batch of nb_alloc pairs keeps its CRP words (0.5 MB per pair at
   // 2000 frames) so the one-wave-per-pair DP launch is wide enough; the CRP itself runs in

@@ -28,6 +28,8 @@ namespace acoss {
 namespace {
 
 constexpr int kMS = 9;
+// 16-bit prefix of "no element": above every real prefix (finite keys >= +0 have prefixes <= 0x7f80)
+constexpr unsigned kNone = 0x7fffu;
 
 #ifdef ACOSS_STAMPS  // diagnostic builds only: per-phase cycle sums of the fused sweep
 __device__ unsigned long long d_sweep_stamps[32];
@@ -457,7 +459,8 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
         if (FAST || r < rows) st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), key >> 16);
         hrow += ldr;  // next row: one scalar add instead of 32 hoisted row pointers
         asm volatile("" : "+s"(hrow));
-        tileT[(t + r) * kTP + spos(r)] = (uint16_t)(key >> 16);
+        // rows past M' in the last strip: kNone in the column plane (no tail mask in the select)
+        tileT[(t + r) * kTP + spos(r)] = (uint16_t)(FAST || r < rows ? key >> 16 : kNone);
       }
     }
     }  // !FAST
@@ -497,6 +500,14 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
       ACOSS_STAMP_ADD(3, t3, t4);  // column-plane stores, barrier, roll
     }
   }
+  // kNone over [N', align32(N')) of every row: the row select's last 32-element run then needs
+  // no tail mask. After the barrier, so it lands after the walk's out-of-range stores there.
+  __syncthreads();
+  const int padw = (int)((V.Np + 31) & ~31) - V.Np;
+  for (int e = t; e < kSR * 32; e += kSW) {
+    const int r = e >> 5, c = e & 31;
+    if (c < padw && r < rows) Hr[(size_t)r * ldr + V.Np + c] = (uint16_t)kNone;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride) {
@@ -519,7 +530,6 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
 // 2h+1 in bits 16..31. Real prefixes are <= 0x7f80 (keys are >= +0, the sign bit is 0), so
 // 0x7fff marks "no element" and every field keeps a free guard bit for SWAR arithmetic.
 // ---------------------------------------------------------------------------------------
-constexpr unsigned kNone = 0x7fffu;
 
 __device__ __forceinline__ unsigned pk_min_u16(unsigned a, unsigned b) {
   typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -578,15 +588,11 @@ struct Line {
       for (int h = 0; h < KPL / 2; ++h)  // (element h, element h + 16) from natural pairs
         pv[h] = __builtin_amdgcn_perm(w[8 + (h >> 1)], w[h >> 1], (h & 1) ? 0x07060302u : 0x05040100u);
     }
-    if (base + KPL > n) {
-      int nv = n - base;  // opaque per call: no hoisted per-element predicates in callers' loops
-      asm volatile("" : "+v"(nv));
+    // the planes hold kNone past the line's end inside the last run (the sweep stores it), so
+    // only lanes wholly past the line need filling
+    if (base >= n) {
 #pragma unroll
-      for (int h = 0; h < KPL / 2; ++h) {
-        const unsigned a = (h < nv) ? (pv[h] & 0xffffu) : kNone;
-        const unsigned b = (h + 16 < nv) ? (pv[h] >> 16) : kNone;
-        pv[h] = a | (b << 16);
-      }
+      for (int h = 0; h < KPL / 2; ++h) pv[h] = kNone * 0x10001u;
     }
   }
   // #elements <= x (x <= 0x7fff): per field (x + 0x8000) - a keeps bit 15 iff a <= x, with no

@@ -121,3 +121,23 @@ print("ok")
     env = dict(os.environ, ACOSS_CRP_PATH=path)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_crp_align_run_edges():
+    """Split path at line lengths on the 32-element run and 256-column panel edges
+    (N' = 32, 33, 289, 1280, 1281, 2016, 2017, 2048): the planes' kNone pads past N' replace the
+    selects' tail masks, so every partial run must read as "no element"."""
+    rng = np.random.Generator(np.random.PCG64(5))
+    tracks = []
+    for n in [41, 42, 298, 1289, 1290, 2025, 2026, 2057]:
+        x = synthetic.render(rng, synthetic.base_sequence(rng, n))
+        if n > 1000:
+            x[100:160] = 0.0
+        tracks.append(x)
+    feats, off, lens = synthetic.pack(tracks)
+    pairs = np.array([(i, j) for i in range(len(tracks)) for j in range(len(tracks)) if i != j], np.int32)
+    q, d, k = oracle.crp_batch(feats, off, lens, pairs)
+    got = _lib.crp_align(feats, off, lens, int(lens.max()), pairs, _lib.crp_params(), qmax=True, dmax=True, oti=True)
+    np.testing.assert_array_equal(got["oti"].cpu().numpy(), k)
+    np.testing.assert_array_equal(got["qmax"].cpu().numpy(), q)
+    np.testing.assert_array_equal(got["dmax"].cpu().numpy(), d)
