@@ -510,6 +510,192 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// MFMA sweep (FAST strips: tau == 1, a full 32-row strip, all 40 query frames in the track).
+// Per panel of kMW diagonals, the Gram terms G(i0 + k, j0 + c) of the panel's parallelogram
+// (0 <= c - k < kMW, k < 40) come from v_mfma_f32_16x16x4f32 tiles: three chained MFMAs over
+// the 12 bins accumulate exactly as the canonical fmaf chain (bins 0..11 from +0), bit for bit
+// (measured on gfx950: profiles/r02/mfma_probe_r02.txt). The tiles land in LDS diagonal-major,
+// Gd[d][k] = G(i0 + k, j0 + d + k); lane d of a wave then walks its diagonal's 16-row half with
+// the 9-term window sums in registers (packed rows r, r + 1, the canonical sequential order),
+// and emits the prefixes exactly as the VALU walk does. The VALU keeps only the window sums and
+// the emits; the LDS carries 4 B per Gram term instead of the 48-B reference frame per term.
+// ---------------------------------------------------------------------------------------
+constexpr int kMW = 128;                  // diagonals per panel
+constexpr int kMCols = kMW + kSR;         // 160 columns touched per panel
+constexpr int kDP = 44;                   // floats per diagonal in Gd (40 used; 44: conflict-free b128 reads)
+constexpr int kMfmaLds = (kMW * kDP + kMCols) * 4 + kMCols * kTP * 2;
+
+typedef float f32x4m __attribute__((ext_vector_type(4)));
+
+// Window sums and emits of rows R0 .. R0 + 15 on diagonal dw (cells (R0 + r, j0 + dw + R0 + r)).
+// EDGE: some columns fall outside [0, N') (first / last panels): their stores go to the pad column.
+template <bool EDGE>
+__device__ __forceinline__ void mfma_walk(const PairView& V, int i0, int j0, int dw, int R0, const float* Gd,
+                                          const float* Ns, uint16_t* tileT, uint16_t* Hr, int ldr) {
+  float g[24];  // G(i0 + R0 + k, j0 + dw + R0 + k), k < 24
+  const f32x4m* src = reinterpret_cast<const f32x4m*>(Gd + dw * kDP + R0);
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const f32x4m v = src[q];
+    g[4 * q] = v.x;
+    g[4 * q + 1] = v.y;
+    g[4 * q + 2] = v.z;
+    g[4 * q + 3] = v.w;
+  }
+  const float* Nq0 = V.NXq + i0 + R0;
+  auto nqr = [&](int r) {  // row norm: a scalar load at a compile-time offset
+    const float* base = Nq0;
+    asm volatile("" : "+s"(base));
+    return *(const __attribute__((address_space(4))) float*)(base + r);
+  };
+  gu16* hrow = (gu16*)(Hr + (size_t)R0 * ldr);
+  // tileT[(dw + R0 + r) * kTP + spos(R0 + r)], spos(R0 + r) = 2 r + R0 / 16 for r < 16
+  uint16_t* tt = tileT + (dw + R0) * kTP + (R0 >> 4);
+  const int col0 = j0 + dw + R0;
+  const float* ns = Ns + dw + R0;
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    f32x2 dot = f32x2{g[r], g[r + 1]};
+#pragma unroll
+    for (int u = 1; u < kMS; ++u) dot = dot + f32x2{g[r + u], g[r + u + 1]};
+    const f32x2 nq = f32x2{nqr(r), nqr(r + 1)};
+    const f32x2 ny = f32x2{ns[r], ns[r + 1]};
+    const f32x2 d2 = pk_fma(f32x2{-2.0f, -2.0f}, dot, nq) + ny;  // nq - 2 dot exactly (2 dot is exact)
+    const unsigned k0 = __builtin_bit_cast(unsigned, d2.x > 0.0f ? d2.x : 0.0f);
+    const unsigned k1 = __builtin_bit_cast(unsigned, d2.y > 0.0f ? d2.y : 0.0f);
+    const int col = col0 + r;
+    if (EDGE) {
+      st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), k0 >> 16);
+      st_u16(hrow, ldr + min((unsigned)(col + 1), (unsigned)(ldr - 1)), k1 >> 16);
+    } else {
+      st_u16(hrow, (unsigned)col, k0 >> 16);
+      st_u16(hrow, ldr + (unsigned)(col + 1), k1 >> 16);
+    }
+    hrow += 2 * ldr;
+    asm volatile("" : "+s"(hrow));
+    tt[r * (kTP + 2)] = (uint16_t)(k0 >> 16);
+    tt[(r + 1) * (kTP + 2)] = (uint16_t)(k1 >> 16);
+  }
+}
+
+__device__ __forceinline__ void sweep_body_mfma(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr,
+                                                int ldc, int64_t kstride, float* Gd, float* Ns, uint16_t* tileT) {
+  const int i0 = strip * kSR;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
+  uint16_t* Hc = K.hc + (size_t)p * kstride;
+  const int li = lane & 15, lk = lane >> 4;
+  // A fragments: query frame i0 + 16 rt + li (rows >= 40 clamped: computed, never stored),
+  // bins 4 s + lk; fixed for the whole strip
+  float a[3][3];
+#pragma unroll
+  for (int rt = 0; rt < 3; ++rt) {
+    const int f = min(i0 + 16 * rt + li, V.nq - 1);
+#pragma unroll
+    for (int s2 = 0; s2 < 3; ++s2) a[rt][s2] = V.X[(size_t)f * 12 + 4 * s2 + lk];
+  }
+  const int dw = 64 * (w & 1) + lane;  // this lane's diagonal in the walk
+  const int R0 = 16 * (w >> 1);        // first row of its half-strip
+  // B fragments of this wave's column tiles ct = w + 4 m (m < 3, ct < 11): reference frame
+  // j0 + 16 ct + li (clamped: out-of-range columns are computed, never stored), bins 4 s + lk.
+  // The next panel's are loaded during this panel's walk.
+  auto load_b = [&](int jn, float (&bf)[3][3]) {
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int f = min(max(jn + 16 * (w + 4 * m) + li, 0), V.nr - 1);
+      const float* y = V.Yr + (size_t)f * 12 + lk;
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) bf[m][s2] = y[4 * s2];
+    }
+  };
+  // Gd element of (k, c): (c - k) * kDP + k; this lane's part, c = 16 ct + li, k = 16 rt + 4 lk + i
+  float* gl = Gd + (16 * w + li) * kDP - (kDP - 1) * 4 * lk;
+  const bool k_ok2 = lk < 2;  // row tile 2 holds rows 32..47: only k < 40 is stored
+  float bc[3][3], bn[3][3];
+  load_b(-(kSR - 1), bc);
+  for (int j0 = -(kSR - 1); j0 < V.Np; j0 += kMW) {
+    ACOSS_STAMP(t0);
+    // (the previous panel's walk, copy-out and roll are behind the barriers below)
+    for (int b = t; b < kMCols; b += kSW) {
+      const int jr = j0 + b;
+      Ns[b] = (jr >= 0 && jr < V.Np) ? V.NXr[jr] : 0.0f;
+    }
+    // Gram tiles (rt, ct) with rt <= ct <= rt + 8: three chained MFMAs per tile, the row tiles
+    // of one column tile interleaved so consecutive MFMAs are independent
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int ct = w + 4 * m;  // wave-uniform
+      if (ct >= 11) continue;
+      const bool v0 = ct <= 8, v1 = ct >= 1 && ct <= 9, v2 = ct >= 2;
+      f32x4m acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = acc0, acc2 = acc0;
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) {
+        if (v0) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][s2], bc[m][s2], acc0, 0, 0, 0);
+        if (v1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1][s2], bc[m][s2], acc1, 0, 0, 0);
+        if (v2) acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2][s2], bc[m][s2], acc2, 0, 0, 0);
+      }
+      // d = 16 (ct - rt) + li - 4 lk - i: always in [1, 127] for 1 <= ct - rt <= 7; the edge
+      // tiles (ct - rt = 0 or 8) keep d >= 0 / d < kMW per element
+      float* gm = gl + 16 * 4 * m * kDP;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int dl = li - 4 * lk - i;
+        // row tile 0: k = 4 lk + i, d = 16 ct + dl
+        if (v0 && (ct == 0 ? dl >= 0 : (ct == 8 ? dl < 0 : true)))
+          gm[-(kDP - 1) * i] = acc0[i];
+        if (v1 && (ct == 1 ? dl >= 0 : (ct == 9 ? dl < 0 : true)))
+          gm[-16 * kDP + 16 - (kDP - 1) * i] = acc1[i];
+        if (v2 && k_ok2 && (ct == 2 ? dl >= 0 : (ct == 10 ? dl < 0 : true)))
+          gm[-32 * kDP + 32 - (kDP - 1) * i] = acc2[i];
+      }
+    }
+    ACOSS_STAMP(t1);
+    __syncthreads();  // Gd, Ns and the rolled tileT tail are in place
+    ACOSS_STAMP(t2);
+    if (j0 + kMW < V.Np) load_b(j0 + kMW, bn);
+    if (j0 < 0 || j0 + kMCols > V.Np)
+      mfma_walk<true>(V, i0, j0, dw, R0, Gd, Ns, tileT, Hr, ldr);
+    else
+      mfma_walk<false>(V, i0, j0, dw, R0, Gd, Ns, tileT, Hr, ldr);
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) bc[m][s2] = bn[m][s2];
+    ACOSS_STAMP(t3);
+    __syncthreads();
+    // columns [j0, j0 + kMW) complete: strip-major prefixes, 64 B per column
+    if (t < kMW) {
+      const int jj = j0 + t;
+      if (jj >= 0 && jj < V.Np) {
+        const uint32_t* srcw = reinterpret_cast<const uint32_t*>(tileT + t * kTP);
+        uint4* dh = reinterpret_cast<uint4*>(Hc + ((size_t)strip * ldc + jj) * kSR);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dh[q] = make_uint4(srcw[4 * q], srcw[4 * q + 1], srcw[4 * q + 2], srcw[4 * q + 3]);
+      }
+    }
+    __syncthreads();
+    // roll the 31-column tail to the front (16 used words per column)
+    for (int e = t; e < (kSR - 1) * 16; e += kSW) {
+      const int c2 = e >> 4, w2 = e & 15;
+      reinterpret_cast<uint32_t*>(tileT)[c2 * (kTP / 2) + w2] = reinterpret_cast<const uint32_t*>(tileT)[(kMW + c2) * (kTP / 2) + w2];
+    }
+    ACOSS_STAMP(t4);
+    ACOSS_STAMP_ADD(0, t0, t1);  // norms + Gram tiles
+    ACOSS_STAMP_ADD(1, t1, t2);  // barrier before the walk
+    ACOSS_STAMP_ADD(2, t2, t3);  // walk
+    ACOSS_STAMP_ADD(3, t3, t4);  // barrier, column-plane stores, barrier, roll
+  }
+  // kNone over [N', align32(N')) of every row (see sweep_body)
+  __syncthreads();
+  const int padw = (int)((V.Np + 31) & ~31) - V.Np;
+  for (int e = t; e < kSR * 32; e += kSW) {
+    const int r = e >> 5, c = e & 31;
+    if (c < padw) Hr[(size_t)r * ldr + V.Np + c] = (uint16_t)kNone;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride) {
   __shared__ __attribute__((aligned(16))) float Ys[kYsFloats];
   __shared__ float Ns[kSCols];
@@ -1105,12 +1291,13 @@ __global__ __launch_bounds__(512, 4) void k_sel_rows9(CrpBatch B, KeyPlanes K, i
 // fewer). LDS of the two phases is one union.
 constexpr int kSweepLds = (kYsFloats + kSCols) * 4 + kSCols * kTP * 2;
 constexpr int kRowsLds = 4 * (int)sizeof(WaveLds) + kSR * 64 * 4;
-constexpr int kFusedLds = kSweepLds > kRowsLds ? kSweepLds : kRowsLds;
+constexpr int kFusedLds0 = kSweepLds > kRowsLds ? kSweepLds : kRowsLds;
+constexpr int kFusedLds = kFusedLds0 > kMfmaLds ? kFusedLds0 : kMfmaLds;
 
 __global__ __launch_bounds__(256, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride,
                                                      float kappa, float* __restrict__ thr, float* __restrict__ Tq,
                                                      int64_t thr_stride, uint32_t* __restrict__ RT, int64_t rt_stride,
-                                                     int ld) {
+                                                     int ld, int use_mfma) {
   __shared__ __attribute__((aligned(16))) char smem[kFusedLds];
   float* Ys = reinterpret_cast<float*>(smem);
   float* Ns = Ys + kYsFloats;
@@ -1119,10 +1306,16 @@ __global__ __launch_bounds__(256, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K,
   const PairView V = pair_view(B, p);
   const int strip = blockIdx.x, i0 = strip * kSR;
   if (i0 >= V.Mp || V.Np <= 0) return;
-  if (V.tau == 1 && i0 + kSR <= V.Mp && i0 + kSR + kMS - 1 <= V.nq)
-    sweep_body<true>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
-  else
+  if (V.tau == 1 && i0 + kSR <= V.Mp && i0 + kSR + kMS - 1 <= V.nq) {
+    if (use_mfma)
+      sweep_body_mfma(V, p, strip, K, ldr, ldc, kstride, reinterpret_cast<float*>(smem),
+                      reinterpret_cast<float*>(smem) + kMW * kDP,
+                      reinterpret_cast<uint16_t*>(reinterpret_cast<float*>(smem) + kMW * kDP + kMCols));
+    else
+      sweep_body<true>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
+  } else {
     sweep_body<false>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
+  }
   ACOSS_STAMP(r0);
   __syncthreads();  // the strip's F rows are complete (block-scope visibility of the global stores)
 #ifdef ACOSS_ABL_NOROWS  // timing ablation only (wrong results): sweep without the row select
@@ -1222,10 +1415,16 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
     const char* e = getenv("ACOSS_FUSE_ROWS");
     return !(e && strcmp(e, "0") == 0);
   }();
+  // Gram on the packed-FP32 VALU walk (default) or on MFMA (ACOSS_SWEEP=mfma): identical keys;
+  // the MFMA sweep measured 15 % slower
+  static const bool sweep_mfma = [] {
+    const char* e = getenv("ACOSS_SWEEP");
+    return e && strcmp(e, "mfma") == 0;
+  }();
   if (fused) {
     prof_begin(PH_SWEEP, s);
     hipLaunchKernelGGL(k_sweep_rows9, dim3(nstrips, nb), dim3(256), 0, s, B, K, ldk, ldk, kstride, kappa, thr_r, T_r,
-                       thr_stride, RT, mask_stride, ld);
+                       thr_stride, RT, mask_stride, ld, sweep_mfma ? 1 : 0);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_SWEEP, s);
   } else {

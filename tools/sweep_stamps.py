@@ -20,7 +20,7 @@ tracks, _ = corpus_tracks(1, 2000, 20250101)
 bank = ChromaBank(tracks)
 T = len(tracks)
 pairs = torch.as_tensor(np.array([(i, j) for i in range(T) for j in range(i + 1, T)], np.int32)[:4000]).cuda()
-out = (ctypes.c_ulonglong * 16)()
+out = (ctypes.c_ulonglong * 32)()
 bank.crp_align(pairs)
 torch.cuda.synchronize()
 lib.acoss_debug_sweep_stamps(out)
@@ -28,13 +28,8 @@ bank.crp_align(pairs)
 torch.cuda.synchronize()
 lib.acoss_debug_sweep_stamps(out)
 blocks = out[5]
-names = ["fill+2 barriers", "diagonal walk", "barrier after walk", "Hc stores+barrier+roll", "row select"]
+names = ["fill / norms+Gram", "walk (VALU) / barrier", "barrier / walk (MFMA)", "Hc stores+barrier+roll", "row select"]
 tot = sum(out[i] for i in range(5))
+print("mode", os.environ.get("ACOSS_SWEEP", "mfma"), "blocks", blocks)
 for i, nm in enumerate(names):
     print("%-28s %10.0f per wave  %5.1f%%" % (nm, out[i] / blocks / 4, 100.0 * out[i] / tot))
-rows = blocks * 32
-print("row select split (per row): prefix search %.0f, threshold total %.0f, le bits %.0f, transpose/wave %.0f"
-      % (out[9] / rows, out[6] / rows, out[7] / rows, out[8] / blocks / 4))
-cols = max(out[12], 1)
-print("column select (per column): threshold %.0f, le bits + word %.0f  (%d columns)" % (out[10] / cols, out[11] / cols, cols))
-print("blocks", blocks)
