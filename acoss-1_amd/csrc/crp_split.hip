@@ -511,6 +511,142 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
 }
 
 // ---------------------------------------------------------------------------------------
+// Systolic sweep (FAST strips: tau == 1, a full 32-row strip, all 40 query frames in the track).
+// Lane l of a wave holds reference frame jb + l (12 VGPRs) for a whole column block; the
+// strip's 40 query frames arrive as SGPR pairs (scalar loads of the interleaved frame pairs),
+// and one packed-FP32 fmaf chain per step pair gives the lane's Gram terms G(i0 + kk, jb + l),
+// G(i0 + kk + 1, jb + l) in the canonical order. The 9-term window of cell (r, c) starts on
+// lane c - jb at step r and moves one lane per step (v_add_f32 with a DPP wave_shr:1 operand),
+// collecting G(r + u, c + u) in the canonical sequential order; it completes on lane
+// c - jb + 8 at step r + 8. Lanes 0..7 finish windows that began left of the block and are
+// dropped: kSysCols = 56 valid columns per 64 lanes. No LDS and no barriers: each lane owns
+// its output column's 32 rows, so the strip-major prefixes leave straight from registers (split
+// word order) and a step's row-major prefixes are 56 consecutive columns.
+// ---------------------------------------------------------------------------------------
+constexpr int kSysCols = 56;
+
+__device__ __forceinline__ float dpp_shr1(float v) {  // lane l <- lane l - 1 (lane 0 <- 0)
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
+}
+
+__device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr,
+                                               int ldc, int64_t kstride) {
+  constexpr int kSteps = kSR + kMS - 1;  // 40
+  const int i0 = strip * kSR;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
+  uint16_t* Hc = K.hc + (size_t)p * kstride;
+  const float* X2b = V.X2 + (size_t)i0 * 24;
+  const float* Nq0 = V.NXq + i0;
+  auto nqr = [&](int r) {  // row norm: a scalar load at a compile-time offset
+    const float* base = Nq0;
+    asm volatile("" : "+s"(base));
+    return *(const __attribute__((address_space(4))) float*)(base + r);
+  };
+  auto xpair = [&](int kk, f32x2 (&x)[12]) {  // (X_{i0+kk}[b], X_{i0+kk+1}[b]), scalar loads
+    const float* base = X2b;
+    asm volatile("" : "+s"(base));
+    const cfloat4* q = (const cfloat4*)(base + kk * 24);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const f32x4 v = q[c];
+      x[2 * c] = f32x2{v.x, v.y};
+      x[2 * c + 1] = f32x2{v.z, v.w};
+    }
+  };
+  auto load_y = [&](int jb, f32x4 (&y)[3]) {
+    const int f = min(jb + lane, V.nr - 1);  // frames past the track: only dropped cells use them
+    const f32x4* src = reinterpret_cast<const f32x4*>(V.Yr + (size_t)f * 12);
+    y[0] = src[0];
+    y[1] = src[1];
+    y[2] = src[2];
+  };
+  const int nblk = (V.Np + kSysCols - 1) / kSysCols;
+  f32x4 ynext[3];
+  if (w < nblk) load_y(w * kSysCols, ynext);
+#pragma unroll 1
+  for (int cb = w; cb < nblk; cb += 4) {
+    const int jb = cb * kSysCols;
+    float y[12];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      y[4 * q] = ynext[q].x;
+      y[4 * q + 1] = ynext[q].y;
+      y[4 * q + 2] = ynext[q].z;
+      y[4 * q + 3] = ynext[q].w;
+    }
+    if (cb + 4 < nblk) load_y(jb + 4 * kSysCols, ynext);
+    // this lane's output column; dropped lanes and columns past N' store to the pad column
+    const int col = jb + lane - (kMS - 1);
+    const bool valid = lane >= kMS - 1 && col < V.Np;
+    const unsigned hcol = valid ? (unsigned)col : (unsigned)(ldr - 1);
+    const float ny = valid ? V.NXr[col] : 0.0f;
+    gu16* hrow = (gu16*)Hr;
+    float A[kMS];  // A[u]: window of row kk - u after u + 1 terms
+    unsigned kh[16];    // rows 0..15: full keys until their split partner (row + 16) is done
+    unsigned hw[16];    // split-order words: rows (h, h + 16)
+    f32x2 xb[12];
+    xpair(0, xb);
+#pragma unroll
+    for (int kk = 0; kk < kSteps; kk += 2) {
+      f32x2 g2 = pk_fma(xb[0], f32x2{y[0], y[0]}, f32x2{0.0f, 0.0f});
+#pragma unroll
+      for (int b = 1; b < 12; ++b) g2 = pk_fma(xb[b], f32x2{y[b], y[b]}, g2);
+      if (kk + 2 < kSteps) xpair(kk + 2, xb);
+      float dots[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = kk + h;
+        const float g = h ? g2.y : g2.x;
+#pragma unroll
+        for (int u = kMS - 1; u >= 1; --u) {
+          const int r = k - u;
+          if (r >= 0 && r < kSR) A[u] = dpp_shr1(A[u - 1]) + g;
+        }
+        if (k < kSR) A[0] = g;
+        dots[h] = A[kMS - 1];
+      }
+      const int r = kk - (kMS - 1);  // rows r, r + 1 complete on this step pair
+      if (r >= 0) {
+        const f32x2 nq = f32x2{nqr(r), nqr(r + 1)};
+        const f32x2 d2 = pk_fma(f32x2{-2.0f, -2.0f}, f32x2{dots[0], dots[1]}, nq) + f32x2{ny, ny};
+        const unsigned k0 = __builtin_bit_cast(unsigned, d2.x > 0.0f ? d2.x : 0.0f);
+        const unsigned k1 = __builtin_bit_cast(unsigned, d2.y > 0.0f ? d2.y : 0.0f);
+        st_u16(hrow, hcol, k0 >> 16);
+        st_u16(hrow, (unsigned)ldr + hcol, k1 >> 16);
+        hrow += 2 * ldr;
+        asm volatile("" : "+s"(hrow));
+        if (r < 16) {
+          kh[r] = k0;
+          kh[r + 1] = k1;
+        } else {
+          hw[r - 16] = __builtin_amdgcn_perm(k0, kh[r - 16], 0x07060302u);
+          hw[r - 15] = __builtin_amdgcn_perm(k1, kh[r - 15], 0x07060302u);
+        }
+      }
+    }
+#ifdef ACOSS_ABL_NOHC  // timing ablation only (wrong results): no strip-major plane stores
+    if (hw[0] == 0x12345678u && hw[15] == 0x9abcdef0u) {
+#else
+    if (valid) {
+#endif
+      uint4* dh = reinterpret_cast<uint4*>(Hc + ((size_t)strip * ldc + col) * kSR);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dh[q] = make_uint4(hw[4 * q], hw[4 * q + 1], hw[4 * q + 2], hw[4 * q + 3]);
+    }
+  }
+  // kNone over [N', align32(N')) of every row (see sweep_body); the walk's stores above went
+  // to valid columns or the pad column only
+  __syncthreads();
+  const int padw = (int)((V.Np + 31) & ~31) - V.Np;
+  for (int e = threadIdx.x; e < kSR * 32; e += kSW) {
+    const int r = e >> 5, c = e & 31;
+    if (c < padw) Hr[(size_t)r * ldr + V.Np + c] = (uint16_t)kNone;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // MFMA sweep (FAST strips: tau == 1, a full 32-row strip, all 40 query frames in the track).
 // Per panel of kMW diagonals, the Gram terms G(i0 + k, j0 + c) of the panel's parallelogram
 // (0 <= c - k < kMW, k < 40) come from v_mfma_f32_16x16x4f32 tiles: three chained MFMAs over
@@ -1307,7 +1443,9 @@ __global__ __launch_bounds__(256, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K,
   const int strip = blockIdx.x, i0 = strip * kSR;
   if (i0 >= V.Mp || V.Np <= 0) return;
   if (V.tau == 1 && i0 + kSR <= V.Mp && i0 + kSR + kMS - 1 <= V.nq) {
-    if (use_mfma)
+    if (use_mfma == 2)
+      sweep_body_sys(V, p, strip, K, ldr, ldc, kstride);
+    else if (use_mfma)
       sweep_body_mfma(V, p, strip, K, ldr, ldc, kstride, reinterpret_cast<float*>(smem),
                       reinterpret_cast<float*>(smem) + kMW * kDP,
                       reinterpret_cast<uint16_t*>(reinterpret_cast<float*>(smem) + kMW * kDP + kMCols));
@@ -1415,16 +1553,18 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
     const char* e = getenv("ACOSS_FUSE_ROWS");
     return !(e && strcmp(e, "0") == 0);
   }();
-  // Gram on the packed-FP32 VALU walk (default) or on MFMA (ACOSS_SWEEP=mfma): identical keys;
-  // the MFMA sweep measured 15 % slower
-  static const bool sweep_mfma = [] {
+  // FAST strips: the systolic walk (default), the LDS-fed packed-FP32 diagonal walk
+  // (ACOSS_SWEEP=valu) or the MFMA Gram tiles (ACOSS_SWEEP=mfma); identical keys
+  static const int sweep_mfma = [] {
     const char* e = getenv("ACOSS_SWEEP");
-    return e && strcmp(e, "mfma") == 0;
+    if (e && strcmp(e, "mfma") == 0) return 1;
+    if (e && strcmp(e, "valu") == 0) return 0;
+    return 2;
   }();
   if (fused) {
     prof_begin(PH_SWEEP, s);
     hipLaunchKernelGGL(k_sweep_rows9, dim3(nstrips, nb), dim3(256), 0, s, B, K, ldk, ldk, kstride, kappa, thr_r, T_r,
-                       thr_stride, RT, mask_stride, ld, sweep_mfma ? 1 : 0);
+                       thr_stride, RT, mask_stride, ld, sweep_mfma);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_SWEEP, s);
   } else {
