@@ -32,7 +32,7 @@ constexpr int kMS = 9;
 constexpr unsigned kNone = 0x7fffu;
 
 #ifdef ACOSS_STAMPS  // diagnostic builds only: per-phase cycle sums of the fused sweep
-__device__ unsigned long long d_sweep_stamps[32];
+__device__ unsigned long long d_sweep_stamps[48];
 __device__ __forceinline__ unsigned long long sstamp() {
   unsigned long long t;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -524,6 +524,9 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
 // word order) and a step's row-major prefixes are 56 consecutive columns.
 // ---------------------------------------------------------------------------------------
 constexpr int kSysCols = 56;
+#ifndef ACOSS_SYS_WPE
+#define ACOSS_SYS_WPE 6
+#endif
 
 __device__ __forceinline__ float dpp_shr1(float v) {  // lane l <- lane l - 1 (lane 0 <- 0)
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
@@ -832,7 +835,9 @@ __device__ __forceinline__ void sweep_body_mfma(const PairView& V, int p, int st
   }
 }
 
-__global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride) {
+// edge_only: FAST strips are left to k_sweep_sys9 (unfused systolic path)
+__global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride,
+                                                int edge_only) {
   __shared__ __attribute__((aligned(16))) float Ys[kYsFloats];
   __shared__ float Ns[kSCols];
   __shared__ __attribute__((aligned(16))) uint16_t tileT[kSCols * kTP];  // [column][row] 16-bit prefixes
@@ -840,10 +845,21 @@ __global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr
   const PairView V = pair_view(B, p);
   const int strip = blockIdx.x, i0 = strip * kSR;
   if (i0 >= V.Mp || V.Np <= 0) return;
-  if (V.tau == 1 && i0 + kSR <= V.Mp && i0 + kSR + kMS - 1 <= V.nq)
-    sweep_body<true>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
-  else
+  if (V.tau == 1 && i0 + kSR <= V.Mp && i0 + kSR + kMS - 1 <= V.nq) {
+    if (!edge_only) sweep_body<true>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
+  } else {
     sweep_body<false>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
+  }
+}
+
+// Systolic sweep of the FAST strips alone (no LDS): high occupancy while its stores drain.
+__global__ __launch_bounds__(256, ACOSS_SYS_WPE) void k_sweep_sys9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
+                                                                   int64_t kstride) {
+  const int p = blockIdx.y;
+  const PairView V = pair_view(B, p);
+  const int strip = blockIdx.x, i0 = strip * kSR;
+  if (i0 >= V.Mp || V.Np <= 0) return;
+  if (V.tau == 1 && i0 + kSR <= V.Mp && i0 + kSR + kMS - 1 <= V.nq) sweep_body_sys(V, p, strip, K, ldr, ldc, kstride);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1225,7 +1241,19 @@ __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF&
   if (!hinted) L.min_max(&kmin, &kmax);
   int le, less;
   int passes = 0;
+  ACOSS_STAMP(ts0);
+#ifdef ACOSS_ABL_SEARCH2X  // timing ablation only: the search runs twice (same answer)
+  {
+    unsigned h2 = hint->P, a2 = kmin;
+    asm volatile("" : "+s"(h2), "+s"(a2));
+    int le2, less2, p2 = 0;
+    const unsigned P2 = prefix_of_rank(L, lo, a2, kmax, n, h2, &le2, &less2, &p2);
+    asm volatile("" ::"s"(P2), "s"(le2), "s"(less2));
+  }
+#endif
   const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, hint->P, &le, &less, &passes);
+  ACOSS_STAMP(ts1);
+  ACOSS_STAMP_ADD(KF::kRow ? 36 : 32, ts0, ts1);  // prefix search
   ACOSS_COUNT(KF::kRow ? 6 : 11, 1);
   ACOSS_COUNT(KF::kRow ? 7 : 12, passes);
   if (!hinted) {
@@ -1243,7 +1271,7 @@ __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF&
   // density around the answer: the group at Pl, smoothed over the run
   hint->dens = hinted ? 0.5f * hint->dens + 0.5f * (float)(le - less) : (float)(le - less);
   unsigned vlo, vhi;
-#ifdef ACOSS_ABL_NOGROUP
+#if defined(ACOSS_ABL_NOGROUP) || defined(ACOSS_ABL_NOGROUP2)
   if (true) {
     vlo = vhi = Pl << 16;
   } else
@@ -1263,6 +1291,8 @@ __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF&
       vhi = rank_in_prefix(L, Ph, 0, L.count_le(Ph) - le, keyf, W, c_hi);
     }
   }
+  ACOSS_STAMP(ts2);
+  ACOSS_STAMP_ADD(KF::kRow ? 37 : 33, ts1, ts2);  // group keys and ranks
   const float slo = sqrt_rn(__builtin_bit_cast(float, vlo));
   float th;
   if (lo_f == hi_f) {
@@ -1275,6 +1305,8 @@ __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF&
   }
   *thr = th;
   *T = sq_threshold(th);
+  ACOSS_STAMP(ts3);
+  ACOSS_STAMP_ADD(KF::kRow ? 38 : 34, ts2, ts3);  // threshold arithmetic
 }
 
 // Bits of "key <= T" for the KPL elements of this lane (element e = lane*KPL + q): every
@@ -1287,6 +1319,9 @@ __device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, 
   const unsigned T16 = Tbits >> 16;
   const int lane = threadIdx.x & 63;
   const uint32_t word = L.le_mask(T16);  // kNone is never <= T16 <= 0x7f80
+#ifdef ACOSS_ABL_NOGROUP2  // timing ablation only (wrong results): prefix-only decision
+  return word;
+#endif
   // (selected by value: a pointer to either cached group would put both on the stack)
   const bool lo_hit = c_lo.g >= 0 && c_lo.P == T16, hi_hit = c_hi.g >= 0 && c_hi.P == T16;
   W.words[lane] = 0xffffffffu;
@@ -1515,6 +1550,7 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
     const Line<KPL> L = Lnext;
     if (j + 1 < jend) load_col(Lnext, j + 1);
 #endif
+    ACOSS_COUNT(31, 1);  // columns
     // this column's row-threshold word, requested now and used after the select
     const size_t w = (size_t)p * mask_stride + (size_t)(lane * KPL < V.Mp ? lane : 0) * ld + j;
     const uint32_t rt = RT[w];
@@ -1527,12 +1563,15 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
       thr[(size_t)p * thr_stride + j] = th;
       Tq[(size_t)p * thr_stride + j] = Tc;
     }
+    ACOSS_STAMP(tc0);
 #ifdef ACOSS_ABL_NOLEBITS
     const uint32_t bits = 0;
 #else
     const uint32_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
 #endif
     if (lane * KPL < V.Mp) maskT[w] = bits & rt;
+    ACOSS_STAMP(tc1);
+    ACOSS_STAMP_ADD(35, tc0, tc1);  // le_bits and the CRP word
   }
 }
 
@@ -1569,7 +1608,11 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
     prof_end(PH_SWEEP, s);
   } else {
     prof_begin(PH_SWEEP, s);
-    hipLaunchKernelGGL(k_sweep9, dim3(nstrips, nb), dim3(kSW), 0, s, B, K, ldk, ldk, kstride);
+    if (sweep_mfma == 2) {
+      hipLaunchKernelGGL(k_sweep_sys9, dim3(nstrips, nb), dim3(256), 0, s, B, K, ldk, ldk, kstride);
+      ACOSS_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_sweep9, dim3(nstrips, nb), dim3(kSW), 0, s, B, K, ldk, ldk, kstride, sweep_mfma == 2 ? 1 : 0);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_SWEEP, s);
     prof_begin(PH_SEL_ROWS, s);
@@ -1591,9 +1634,9 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
 #ifdef ACOSS_STAMPS
 extern "C" int acoss_debug_sweep_stamps(unsigned long long* out16) {
   if (hipDeviceSynchronize() != hipSuccess) return ACOSS_E_HIP;
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(acoss::d_sweep_stamps), 32 * sizeof(unsigned long long)) != hipSuccess)
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(acoss::d_sweep_stamps), 48 * sizeof(unsigned long long)) != hipSuccess)
     return ACOSS_E_HIP;
-  unsigned long long z[32] = {};
+  unsigned long long z[48] = {};
   if (hipMemcpyToSymbol(HIP_SYMBOL(acoss::d_sweep_stamps), z, sizeof(z)) != hipSuccess) return ACOSS_E_HIP;
   return ACOSS_OK;
 }

@@ -22,7 +22,7 @@ T = len(tracks)
 allp = np.array([(i, j) for i in range(T) for j in range(i + 1, T)], np.int32)
 sel = np.random.default_rng(0).choice(len(allp), 2000, replace=False)
 pairs = torch.as_tensor(allp[np.sort(sel)]).cuda()
-out = (ctypes.c_ulonglong * 32)()
+out = (ctypes.c_ulonglong * 48)()
 lib.acoss_debug_sweep_stamps(out)
 bank.crp_align(pairs)
 torch.cuda.synchronize()

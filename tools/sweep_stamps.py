@@ -20,7 +20,7 @@ tracks, _ = corpus_tracks(1, 2000, 20250101)
 bank = ChromaBank(tracks)
 T = len(tracks)
 pairs = torch.as_tensor(np.array([(i, j) for i in range(T) for j in range(i + 1, T)], np.int32)[:4000]).cuda()
-out = (ctypes.c_ulonglong * 32)()
+out = (ctypes.c_ulonglong * 48)()
 bank.crp_align(pairs)
 torch.cuda.synchronize()
 lib.acoss_debug_sweep_stamps(out)
@@ -28,8 +28,13 @@ bank.crp_align(pairs)
 torch.cuda.synchronize()
 lib.acoss_debug_sweep_stamps(out)
 blocks = out[5]
+rows = blocks * 32
 names = ["fill / norms+Gram", "walk (VALU) / barrier", "barrier / walk (MFMA)", "Hc stores+barrier+roll", "row select"]
 tot = sum(out[i] for i in range(5))
 print("mode", os.environ.get("ACOSS_SWEEP", "mfma"), "blocks", blocks)
 for i, nm in enumerate(names):
     print("%-28s %10.0f per wave  %5.1f%%" % (nm, out[i] / blocks / 4, 100.0 * out[i] / tot))
+cols = max(out[31], 1)
+print("column select per column: search %.0f  group %.0f  threshold %.0f  le_bits+word %.0f  (%d columns)"
+      % (out[32] / cols, out[33] / cols, out[34] / cols, out[35] / cols, cols))
+print("row select per row: search %.0f  group %.0f  threshold %.0f" % (out[36] / rows, out[37] / rows, out[38] / rows))
