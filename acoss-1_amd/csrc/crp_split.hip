@@ -635,8 +635,16 @@ __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int str
     if (valid) {
 #endif
       uint4* dh = reinterpret_cast<uint4*>(Hc + ((size_t)strip * ldc + col) * kSR);
+#ifdef ACOSS_HC_NT  // streaming stores: the column plane is read back by another kernel, later
+      typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+      u32x4v* dv = reinterpret_cast<u32x4v*>(dh);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        __builtin_nontemporal_store(u32x4v{hw[4 * q], hw[4 * q + 1], hw[4 * q + 2], hw[4 * q + 3]}, dv + q);
+#else
 #pragma unroll
       for (int q = 0; q < 4; ++q) dh[q] = make_uint4(hw[4 * q], hw[4 * q + 1], hw[4 * q + 2], hw[4 * q + 3]);
+#endif
     }
   }
   // kNone over [N', align32(N')) of every row (see sweep_body); the walk's stores above went
@@ -891,10 +899,38 @@ __device__ __forceinline__ uint32_t gather_flags(uint32_t acc, uint32_t s, int h
 // SPLIT order: word h = element h (bits 0..15) and element h + 16 (bits 16..31). In this order
 // the flag bits of a SWAR compare on word h (bits 15 and 31) become mask bits h and h + 16 with
 // one shift and one and-or, so an element mask costs 3 VALU per word.
+__device__ __forceinline__ unsigned pk_subsat_u16(unsigned a, unsigned b) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+
+// Bits h, h + 8, h + 16, h + 24 of the result take the flags (bits 7, 15, 23, 31) of word h.
+__device__ __forceinline__ uint32_t gather_flags8(uint32_t acc, uint32_t s, int h) {
+  return ((s >> (7 - h)) & (0x01010101u << h)) | acc;
+}
+
 template <int KPL>
 struct Line {
   static_assert(KPL == 32, "split word order assumes 32 elements per lane");
   unsigned pv[KPL / 2];
+  // Optional 7-bit window around a hint: w8 holds min(max(prefix - base8, 0), 127) for the
+  // lane's 32 elements, four per word (word h = elements h, h + 8, h + 16, h + 24). For
+  // thresholds in [base8, base8 + 126] it answers count / member / le queries exactly at half
+  // the VALU of the 16-bit words (codes 0 and 127 are the saturated "below" and "above" classes).
+  unsigned w8[KPL / 4];
+  unsigned base8;
+  bool win;
+  __device__ __forceinline__ void build_window(unsigned center) {
+    base8 = center > 63u ? center - 63u : 0u;
+    win = true;
+    const unsigned B2 = base8 * 0x10001u;
+    unsigned c[KPL / 2];
+#pragma unroll
+    for (int h = 0; h < KPL / 2; ++h) c[h] = pk_min_u16(pk_subsat_u16(pv[h], B2), 0x007f007fu);
+#pragma unroll
+    for (int h = 0; h < KPL / 4; ++h) w8[h] = __builtin_amdgcn_perm(c[h + 8], c[h], 0x06020400u);
+  }
+  __device__ __forceinline__ bool in_win(unsigned x) const { return win && x >= base8 && x <= base8 + 126u; }
   __device__ __forceinline__ unsigned pfx(int q) const { return q < 16 ? (pv[q] & 0xffffu) : (pv[q - 16] >> 16); }
   // Lane l's KPL elements start at col0 + l * lane_stride. STORED_SPLIT: the plane holds every
   // run in split order already (the strip-major column plane, written so by the sweep);
@@ -909,6 +945,8 @@ struct Line {
     // conditional loads: hipcc branches around each and waits vmcnt(0) after each (16-32
     // serial L2 round trips per line)
     const uint16_t* src = col0 + (base < n ? (size_t)lane * lane_stride : (size_t)0);
+    win = false;
+    base8 = 0u;
     unsigned w[KPL / 2];
 #pragma unroll
     for (int q = 0; q < KPL / 8; ++q) {
@@ -936,6 +974,13 @@ struct Line {
   // #elements <= x (x <= 0x7fff): per field (x + 0x8000) - a keeps bit 15 iff a <= x, with no
   // borrow across fields; popcount on VALU, one DPP wave sum (no SGPR per compare, no SALU).
   __device__ __forceinline__ int count_le(unsigned x) const {
+    if (in_win(x)) {  // wave-uniform
+      const unsigned X4 = (x - base8 + 0x80u) * 0x01010101u;
+      unsigned c = 0;
+#pragma unroll
+      for (int h = 0; h < KPL / 4; ++h) c = __builtin_popcount((X4 - w8[h]) & 0x80808080u) + c;
+      return wave_sum((int)c);
+    }
     const unsigned X2 = (x + 0x8000u) * 0x10001u;
 #ifdef ACOSS_CNT_ILP
     unsigned c[4] = {0, 0, 0, 0};  // four independent v_bcnt chains
@@ -952,6 +997,13 @@ struct Line {
   // Bit q set iff element q's prefix == P (P <= 0x7f80). Per field, (a ^ P) + 0x7fff keeps bit
   // 15 iff a != P; fields are <= 0x7fff, so nothing carries across.
   __device__ __forceinline__ uint32_t eq_mask(unsigned P) const {
+    if (in_win(P) && (P > base8 || base8 == 0u)) {  // code 0 is exact only when base8 == 0
+      const unsigned PP = (P - base8) * 0x01010101u;
+      uint32_t ne8 = 0;
+#pragma unroll
+      for (int h = 0; h < KPL / 4; ++h) ne8 = gather_flags8(ne8, (w8[h] ^ PP) + 0x7f7f7f7fu, h);
+      return ~ne8;
+    }
     const unsigned PP = P * 0x10001u;
     uint32_t ne = 0;
 #pragma unroll
@@ -960,6 +1012,13 @@ struct Line {
   }
   // Bit q set iff element q's prefix <= x (x <= 0x7fff; kNone is never <= a real x).
   __device__ __forceinline__ uint32_t le_mask(unsigned x) const {
+    if (in_win(x)) {
+      const unsigned X4 = (x - base8 + 0x80u) * 0x01010101u;
+      uint32_t le8 = 0;
+#pragma unroll
+      for (int h = 0; h < KPL / 4; ++h) le8 = gather_flags8(le8, X4 - w8[h], h);
+      return le8;
+    }
     const unsigned X2 = (x + 0x8000u) * 0x10001u;
     uint32_t le = 0;
 #pragma unroll
@@ -1402,7 +1461,10 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
     const int i = i0 + r;
     uint32_t word = 0;
     if (i < V.Mp) {
-      const Line<KPL> L = Lnext;
+      Line<KPL> L = Lnext;
+#ifndef ACOSS_NO_WINDOW8
+      if (hint.P != kNoHint) L.build_window(hint.P);
+#endif
       if (r + 1 < (w + 1) * RPW && i + 1 < V.Mp) load_row(Lnext, i + 1);
       const LineCells<true> keyf{V, i};
       float th, T;
@@ -1547,8 +1609,11 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
   if (j0 < jend) load_col(Lnext, j0);
 #pragma unroll 1
   for (int j = j0; j < jend; ++j) {
-    const Line<KPL> L = Lnext;
+    Line<KPL> L = Lnext;
     if (j + 1 < jend) load_col(Lnext, j + 1);
+#endif
+#ifndef ACOSS_NO_WINDOW8
+    if (hint.P != kNoHint) L.build_window(hint.P);
 #endif
     ACOSS_COUNT(31, 1);  // columns
     // this column's row-threshold word, requested now and used after the select

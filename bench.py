@@ -77,7 +77,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--frames", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=20250101)
-    ap.add_argument("--cpu-sample", type=int, default=192, help="pairs timed on the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=640, help="pairs timed on the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
