@@ -1106,6 +1106,26 @@ struct Hint {
   float dens;
 };
 
+// First guess for a line without a neighbour's answer: the order statistic of the same
+// quantile in a systematic sample of the line, one element per lane (line elements 32 l),
+// found by repeated wave minima. Off by about ten prefix units, it replaces the [min, max]
+// bisection (about nine counts) by a window search from the guess.
+template <int KPL>
+__device__ __forceinline__ unsigned sample_hint(const Line<KPL>& L, int n, float kappa) {
+  const int lane = threadIdx.x & 63;
+  unsigned v = L.pv[0] & 0xffffu;  // kNone on lanes past the line
+  const int ns = min(64, (n + KPL - 1) / KPL);
+  const int k = (int)((float)(n - 1) * kappa * (float)ns / (float)n);
+#pragma unroll 1
+  for (int r = 0; r < k; ++r) {
+    const unsigned m = wave_min_u32(v);
+    const int first = __builtin_ctzll(__ballot(v == m));
+    if (lane == first) v = 0xffffffffu;
+  }
+  const unsigned P = wave_min_u32(v);
+  return P > 0x7f80u ? 0x7f80u : P;
+}
+
 // Scratch of one wave in LDS: element list and 64 bit-words.
 struct WaveLds {
   int list[64];
@@ -1463,6 +1483,9 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
     if (i < V.Mp) {
       Line<KPL> L = Lnext;
 #ifndef ACOSS_NO_WINDOW8
+#ifndef ACOSS_NO_SAMPLE_HINT
+      if (hint.P == kNoHint) hint.P = sample_hint(L, V.Np, kappa);
+#endif
       if (hint.P != kNoHint) L.build_window(hint.P);
 #endif
       if (r + 1 < (w + 1) * RPW && i + 1 < V.Mp) load_row(Lnext, i + 1);
@@ -1613,6 +1636,9 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
     if (j + 1 < jend) load_col(Lnext, j + 1);
 #endif
 #ifndef ACOSS_NO_WINDOW8
+#ifndef ACOSS_NO_SAMPLE_HINT
+    if (hint.P == kNoHint) hint.P = sample_hint(L, V.Mp, kappa);
+#endif
     if (hint.P != kNoHint) L.build_window(hint.P);
 #endif
     ACOSS_COUNT(31, 1);  // columns
