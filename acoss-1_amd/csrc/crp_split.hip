@@ -1593,7 +1593,7 @@ __global__ __launch_bounds__(256, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K,
 // column of a run bisects from its min/max).
 // ---------------------------------------------------------------------------------------
 #ifndef ACOSS_CPW
-#define ACOSS_CPW 4
+#define ACOSS_CPW 2
 #endif
 constexpr int kCPW = ACOSS_CPW;
 #ifndef ACOSS_COLS_WPE
