@@ -997,7 +997,9 @@ int run_mask(const Stage& st, const CrpBatch& B, int nb, int L, int nstrips, con
 // X2 is requested, the interleaved frame pairs (n_tracks x ldn x 24).
 int run_prep(const float* feats, const int64_t* off, const int32_t* len, int n_tracks, int max_len, int m, int tau,
              hipStream_t s, float** prof, float** NX, int* ldn, float** X2 = nullptr) {
-  *ldn = (int)align_up((size_t)max_len, 64);
+  // 32 spare frames per track: the systolic sweep's last (partial) strip reads query frames up
+  // to 31 past the track's end (values unused: those rows are never stored)
+  *ldn = (int)align_up((size_t)max_len + 32, 64);
   const size_t base = align_up((size_t)n_tracks * 12 + (size_t)n_tracks * (*ldn), 64);
   const size_t bytes = (base + (X2 ? (size_t)n_tracks * (*ldn) * 24 : 0)) * sizeof(float);
   float* ws = static_cast<float*>(workspace(0, bytes));
@@ -1070,7 +1072,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   const int64_t yrot_stride = (int64_t)align_up((size_t)max_len * 12, 64);
   // split path (one sweep + two line-select kernels, crp_split.hip) needs 16-bit key planes
   static const char* path_env = getenv("ACOSS_CRP_PATH");
-  const bool split = m == 9 && L <= 2048 && !(path_env && strcmp(path_env, "fused") == 0);
+  const bool split = m == 9 && tau == 1 && L <= 2048 && !(path_env && strcmp(path_env, "fused") == 0);
   // row pitch: the selects' 32-element runs end at align32(L); one pad column beyond them takes
   // the sweep's branchless out-of-range stores
   const int ldk = (int)align_up(align_up((size_t)L, 32) + 1, 64);

@@ -1,23 +1,24 @@
-// crp_split.hip — Serra09/Chen CRP in three kernels around ONE distance sweep (m = 9).
+// crp_split.hip — Serra09/Chen CRP (m = 9, tau = 1) in two kernels around ONE distance sweep.
 //
 // Replaces, per pair, the body of essentia ChromaCrossSimilarity (rqa_serra09.py:60-66,
 // latefusion_chen.py:63-69): stacked distances, percentile(row/column, 9.5) and the mutual
 // binary mask, bit-identical to oracle/crp_oracle.cpp.
 //
-//  k_sweep9      one 256-thread block per (32-row strip, pair): diagonal walk (G in
-//                registers, query frames by scalar loads, rolled reference frames in LDS);
-//                every squared-distance key leaves as its HIGH 16 bits only, twice: row-major
-//                Hr[i][j] (straight from registers, 64 lanes = 64 consecutive columns) and
-//                strip-major Hc[i/32][j][i%32] (64 B per column and strip, through a rolling
-//                LDS tile). No full-key plane: 4 B per cell.
-//  k_sel_rows9   (fused into the sweep block as k_sweep_rows9) one wave per CRP row on Hr: the
-//                16-bit prefixes of the two order statistics by a hinted SWAR-count search,
-//                the tied prefix group's exact keys RECOMPUTED (cell_key, one batched round,
-//                ~20-30 cells) and ranked -> percentile -> squared-domain threshold T_row; then
-//                the row's "key <= T_row" bits, transposed in LDS into the strip words RT.
-//  k_sel_cols9   one wave per CRP column on Hc: the same select gives T_col; lane l then holds
-//                rows 32l..32l+31 of the column, i.e. exactly one 32-bit CRP word:
-//                (key <= T_col bits) & RT[strip l][j].
+//  k_sweep_rows9  one 256-thread block per (32-row strip, pair). Systolic walk (no LDS): lane =
+//                 reference column, query frames as SGPR pairs, 9-term diagonal windows carried
+//                 one lane per step by DPP; every squared-distance key leaves as its HIGH 16
+//                 bits only, twice: row-major Hr[i][j] and strip-major Hc[i/32][j][32 rows in
+//                 split word order]. Then the fused row select: one wave per CRP row on Hr, the
+//                 16-bit prefixes of the two order statistics by a hinted SWAR-count search (7-bit
+//                 window codes around the hint), the tied prefix group's exact keys RECOMPUTED
+//                 (cell_key, one batched round, ~20-30 cells) and ranked -> percentile ->
+//                 squared-domain threshold T_row; then the row's "key <= T_row" bits, transposed
+//                 in LDS into the strip words RT.
+//  k_sel_cols9    one wave per CRP column on Hc: the same select gives T_col; lane l then holds
+//                 rows 32l..32l+31 of the column, i.e. exactly one 32-bit CRP word:
+//                 (key <= T_col bits) & RT[strip l][j].
+// The round-1 LDS diagonal walk and the MFMA Gram sweep (bit-exact, slower)
+// were retired in round 2.
 #include <cstdlib>
 #include <cstring>
 
@@ -80,25 +81,6 @@ __device__ __forceinline__ PairView pair_view(const CrpBatch& B, int p) {
 // k_sweep9
 // ---------------------------------------------------------------------------------------
 constexpr int kSR = 32;                       // rows per strip
-constexpr int kSW = 256;                      // diagonals per panel
-constexpr int kSYRows = kSW + kSR + kMS - 2;  // 295 reference frames per panel
-constexpr int kSCols = kSW + kSR;             // 288 columns touched
-constexpr int kSYRowsE = (kSYRows + 1) & ~1;  // 296: whole frame pairs (packed FAST path)
-// Pair block pitch in floats: 24 used + 4 pad. A ds_read_b128 serves 16 lanes per pass; lane
-// pitch 28 dwords puts those 16 lanes on distinct 4-bank groups (pitch 24 would be 2-way).
-constexpr int kYP = 28;
-constexpr int kYsFloats = (kSYRowsE / 2) * kYP > kSYRows * 12 ? (kSYRowsE / 2) * kYP : kSYRows * 12;
-
-__device__ __forceinline__ void load_query(const float* base_ptr, int f, float (&x)[12]) {
-  const float* base = base_ptr + (size_t)f * 12;
-  asm volatile("" : "+s"(base));  // keep each row's scalar load inside the loop
-  const cfloat4* p = (const cfloat4*)base;
-  const f32x4 a = p[0], b = p[1], c = p[2];
-  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-  x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-  x[8] = c.x; x[9] = c.y; x[10] = c.z; x[11] = c.w;
-}
-
 // Key planes of one pair: high 16 bits of every key, row-major (line = CRP row) and
 // strip-major (line = CRP column).
 struct KeyPlanes {
@@ -156,12 +138,6 @@ struct LineCells {
   __device__ __forceinline__ unsigned operator()(int e) const { return cell_key(V, qi(e), rj(e)); }
 };
 
-constexpr int kTP = 34;  // tile pitch in halfwords: 17 words, odd -> lane stride hits distinct banks
-
-// Position of strip row r in a column's 32-row run of the strip-major plane: SPLIT word order
-// (word h = rows h and h + 16, see Line), so the column select loads its words ready to use.
-__device__ __forceinline__ constexpr int spos(int r) { return (r & 15) * 2 + (r >> 4); }
-
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 // Global-address-space u16 pointer: a pointer pinned to SGPRs by an empty asm loses its address
 // space, and generic (flat) stores count in lgkmcnt too, so every s_waitcnt for the LDS reads
@@ -179,337 +155,6 @@ __device__ __forceinline__ void st_u16(gu16* base, unsigned idx, unsigned v) {
 
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-// FAST path diagonal walk in packed FP32 (v_pk_fma_f32 / v_pk_add_f32): lane = diagonal td of
-// the panel, steps kk (query frame i0 + kk) taken two at a time, so one packed chain gives
-// (G_kk, G_kk+1) and one packed window sum gives rows (r, r + 1). Every element follows the
-// scalar canonical order exactly (fused products, sequential sums); only the pairing is new.
-// A wave holds diagonals of one parity PAR: its step pairs (kk, kk + 1) start at kk = PAR mod 2,
-// so reference frames td + kk, td + kk + 1 are always one aligned pair of the interleaved LDS
-// panel Yp; odd waves take step 0 and step 39 alone (rows 0 and 31 alone).
-template <int PAR>
-__device__ __forceinline__ void diag_pk(const PairView& V, int i0, int td, int j0, const float* Yp,
-                                        const float* Ns, uint16_t* tileT, uint16_t* Hr, int ldr) {
-  constexpr int kSteps = kSR + kMS - 1;  // 40
-  const float* X2b = V.X2 + (size_t)i0 * 24;
-  const float* Nq0 = V.NXq + i0;
-  auto nqr = [&](int r) {  // row norm: a scalar load at a compile-time offset
-    const float* base = Nq0;
-    asm volatile("" : "+s"(base));
-    return *(const __attribute__((address_space(4))) float*)(base + r);
-  };
-  auto xpair = [&](int kk, f32x2 (&x)[12]) {  // (X_{i0+kk}[b], X_{i0+kk+1}[b]), scalar loads
-    const float* base = X2b;
-    asm volatile("" : "+s"(base));
-    const cfloat4* q = (const cfloat4*)(base + kk * 24);
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      const f32x4 v = q[c];
-      x[2 * c] = f32x2{v.x, v.y};
-      x[2 * c + 1] = f32x2{v.z, v.w};
-    }
-  };
-  auto yblock = [&](int f, f32x2 (&y)[12]) {  // LDS pair block of panel frames (f, f + 1), f even
-    const f32x4* yp = reinterpret_cast<const f32x4*>(Yp + (f >> 1) * kYP);
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      const f32x4 v = yp[c];
-      y[2 * c] = f32x2{v.x, v.y};
-      y[2 * c + 1] = f32x2{v.z, v.w};
-    }
-  };
-  float G[kSteps];  // fully unrolled: compile-time indices, only a window of them live
-  auto emit = [&](int r, float dot, gu16* hrow) {
-    const float d2 = (nqr(r) - 2.0f * dot) + Ns[td + r];
-    const unsigned key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
-    const int col = j0 + td + r;
-    st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), key >> 16);  // pad column for out-of-range
-    tileT[(td + r) * kTP + spos(r)] = (uint16_t)(key >> 16);
-  };
-  auto emit2 = [&](int r, f32x2 dot, gu16* hrow) {  // rows r, r + 1 (cells on this diagonal)
-    const f32x2 nq = f32x2{nqr(r), nqr(r + 1)};
-    const f32x2 ny = *reinterpret_cast<const f32x2*>(Ns + td + r);  // td + r even: 8-byte aligned
-    const f32x2 d2 = pk_fma(f32x2{-2.0f, -2.0f}, dot, nq) + ny;  // nq - 2 dot exactly (2 dot is exact)
-    const unsigned k0 = __builtin_bit_cast(unsigned, d2.x > 0.0f ? d2.x : 0.0f);
-    const unsigned k1 = __builtin_bit_cast(unsigned, d2.y > 0.0f ? d2.y : 0.0f);
-    const int col = j0 + td + r;
-    st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), k0 >> 16);
-    st_u16(hrow, ldr + min((unsigned)(col + 1), (unsigned)(ldr - 1)), k1 >> 16);
-    tileT[(td + r) * kTP + spos(r)] = (uint16_t)(k0 >> 16);
-    tileT[(td + r + 1) * kTP + spos(r + 1)] = (uint16_t)(k1 >> 16);
-  };
-  auto window1 = [&](int r) {
-    float dot = G[r];
-#pragma unroll
-    for (int u = 1; u < kMS; ++u) dot = dot + G[r + u];
-    return dot;
-  };
-  auto window2 = [&](int r) {
-    f32x2 dot = f32x2{G[r], G[r + 1]};
-#pragma unroll
-    for (int u = 1; u < kMS; ++u) dot = dot + f32x2{G[r + u], G[r + u + 1]};
-    return dot;
-  };
-  gu16* hrow = (gu16*)Hr;
-  auto next_row = [&](int n) {
-    hrow += n * ldr;  // one scalar add per row instead of 32 hoisted row pointers
-    asm volatile("" : "+s"(hrow));
-  };
-  f32x2 xb[12], yb[12];
-  if (PAR == 1) {  // step 0 alone: frame td (odd) is the high half of pair block td - 1
-    xpair(0, xb);
-    yblock(td - 1, yb);
-    float g = __builtin_fmaf(xb[0].x, yb[0].y, 0.0f);
-#pragma unroll
-    for (int b = 1; b < 12; ++b) g = __builtin_fmaf(xb[b].x, yb[b].y, g);
-    G[0] = g;
-  }
-  // software pipeline: step kk + 2's query pair (SMEM) and pair block (LDS) are requested as
-  // soon as step kk's chain has consumed its operands, so their latency overlaps the emits
-  xpair(PAR, xb);
-  yblock(td + PAR, yb);
-#pragma unroll
-  for (int kk = PAR; kk + 1 < kSteps; kk += 2) {
-    f32x2 g = pk_fma(xb[0], yb[0], f32x2{0.0f, 0.0f});
-#pragma unroll
-    for (int b = 1; b < 12; ++b) g = pk_fma(xb[b], yb[b], g);
-    if (kk + 3 < kSteps) {
-      xpair(kk + 2, xb);
-      yblock(td + kk + 2, yb);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    G[kk] = g.x;
-    G[kk + 1] = g.y;
-    // rows completed by this pair: r = kk - 8 and kk - 7
-    const int r = kk - (kMS - 1);
-    if (PAR == 0) {
-      if (r >= 0) {
-        emit2(r, window2(r), hrow);
-        next_row(2);
-      }
-    } else {
-      if (r == -1) {  // row 0 alone (needs G_0 .. G_8)
-        emit(0, window1(0), hrow);
-        next_row(1);
-      } else if (r >= 0) {
-        emit2(r, window2(r), hrow);
-        next_row(2);
-      }
-    }
-  }
-  if (PAR == 1) {  // step 39 alone: frame td + 39 (even) is the low half of its pair block
-    xpair(kSteps - 1, xb);
-    yblock(td + kSteps - 1, yb);
-    float g = __builtin_fmaf(xb[0].x, yb[0].x, 0.0f);
-#pragma unroll
-    for (int b = 1; b < 12; ++b) g = __builtin_fmaf(xb[b].x, yb[b].x, g);
-    G[kSteps - 1] = g;
-    emit(kSR - 1, window1(kSR - 1), hrow);
-  }
-}
-
-// FAST: tau == 1, a full 32-row strip and all 40 query frames inside the track, so the query
-// frames and row norms sit at compile-time offsets from one base (s_load immediates) and no
-// per-row clamp or bound is needed; otherwise the clamped general path.
-template <bool FAST>
-__device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr, int ldc,
-                                           int64_t kstride, float* Ys, float* Ns, uint16_t* tileT) {
-  const int i0 = strip * kSR;
-  const int t = threadIdx.x;
-  const int rows = FAST ? kSR : min(kSR, V.Mp - i0);
-  const float* Xi0 = V.X + (size_t)i0 * 12;
-  const float* Nq0 = V.NXq + i0;
-  auto nqr = [&](int r) {  // row norm: a scalar load at a compile-time offset
-    const float* base = Nq0;
-    asm volatile("" : "+s"(base));
-    return *(const __attribute__((address_space(4))) float*)(FAST ? base + r : V.NXq + min(i0 + r, V.Mp - 1));
-  };
-  uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
-  uint16_t* Hc = K.hc + (size_t)p * kstride;
-  auto query = [&](int kk, float (&x)[12]) {
-    if (FAST) {
-      const float* base = Xi0;
-      asm volatile("" : "+s"(base));  // keep each row's scalar load in the loop
-      const cfloat4* q = (const cfloat4*)(base + kk * 12);
-      const f32x4 a = q[0], b = q[1], c = q[2];
-      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-      x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-      x[8] = c.x; x[9] = c.y; x[10] = c.z; x[11] = c.w;
-    } else {
-      load_query(V.X, min((i0 + kk) * V.tau, V.nq - 1), x);
-    }
-  };
-  // FAST: the next panel's reference frames and norms are fetched into registers while this
-  // panel is swept, and written to LDS after the next barrier (no exposed HBM latency per panel)
-  constexpr int kPF = (kSYRowsE * 3 + kSW - 1) / kSW;  // float4 pieces per thread (4)
-  constexpr int kPN = (kSCols + kSW - 1) / kSW;        // norms per thread (2)
-  f32x4 pf[kPF];
-  float pn[kPN];
-  auto fetch = [&](int j0) {
-#pragma unroll
-    for (int k = 0; k < kPF; ++k) {
-      const int e = t + k * kSW;
-      const int f = e / 3, piece = e - f * 3;
-      const int jr = j0 + f;
-      pf[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      if (e < kSYRowsE * 3 && jr >= 0 && jr < V.nr) pf[k] = reinterpret_cast<const f32x4*>(V.Yr + (size_t)jr * 12)[piece];
-    }
-#pragma unroll
-    for (int k = 0; k < kPN; ++k) {
-      const int b = t + k * kSW, jr = j0 + b;
-      pn[k] = (b < kSCols && jr >= 0 && jr < V.Np) ? V.NXr[jr] : 0.0f;
-    }
-  };
-  if (FAST) fetch(-(kSR - 1));
-  for (int j0 = -(kSR - 1); j0 < V.Np; j0 += kSW) {
-    ACOSS_STAMP(t0);
-    __syncthreads();
-    if (FAST) {  // pair blocks for diag_pk: Ys[f/2][bin][f&1] (tau == 1)
-#pragma unroll
-      for (int k = 0; k < kPF; ++k) {
-        const int e = t + k * kSW;
-        if (e < kSYRowsE * 3) {
-          const int f = e / 3, piece = e - f * 3;
-          float* d = Ys + (f >> 1) * kYP + 8 * piece + (f & 1);
-          d[0] = pf[k].x;
-          d[2] = pf[k].y;
-          d[4] = pf[k].z;
-          d[6] = pf[k].w;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < kPN; ++k)
-        if (t + k * kSW < kSCols) Ns[t + k * kSW] = pn[k];
-    } else {
-      for (int e = t; e < kSYRows * 3; e += kSW) {
-        const int b = e / 3, piece = e - b * 3;
-        const int jr = j0 + b;
-        const int f = jr * V.tau;
-        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (jr >= 0 && f < V.nr) v = reinterpret_cast<const f32x4*>(V.Yr + (size_t)f * 12)[piece];
-        reinterpret_cast<f32x4*>(Ys)[e] = v;
-      }
-    }
-    if (!FAST) {
-      for (int b = t; b < kSCols; b += kSW) {
-        const int jr = j0 + b;
-        Ns[b] = (jr >= 0 && jr < V.Np) ? V.NXr[jr] : 0.0f;
-      }
-    }
-    __syncthreads();
-    ACOSS_STAMP(t1);
-    if (FAST) {
-      if (j0 + kSW < V.Np) fetch(j0 + kSW);
-      const int w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
-      const int td = 128 * (w >> 1) + 2 * lane + (w & 1);  // waves of one diagonal parity
-      if (w & 1)
-        diag_pk<1>(V, i0, td, j0, Ys, Ns, tileT, Hr, ldr);
-      else
-        diag_pk<0>(V, i0, td, j0, Ys, Ns, tileT, Hr, ldr);
-    } else {
-    float gw[kMS];
-    float xb[2][12];
-    f32x4 yb[2][3];
-    query(0, xb[0]);
-    gu16* hrow = (gu16*)Hr;
-    {
-      const f32x4* yp = reinterpret_cast<const f32x4*>(Ys + t * 12);
-      yb[0][0] = yp[0];
-      yb[0][1] = yp[1];
-      yb[0][2] = yp[2];
-    }
-#pragma unroll
-    for (int kk = 0; kk < kSR + kMS - 1; ++kk) {
-      const int cur = kk & 1, nxt = cur ^ 1;
-      if (kk + 1 < kSR + kMS - 1) {
-        query(kk + 1, xb[nxt]);
-        const f32x4* yp = reinterpret_cast<const f32x4*>(Ys + (t + kk + 1) * 12);
-        yb[nxt][0] = yp[0];
-        yb[nxt][1] = yp[1];
-        yb[nxt][2] = yp[2];
-      }
-      const float* x = xb[cur];
-      const f32x4 ya = yb[cur][0], yb1 = yb[cur][1], yc = yb[cur][2];
-      float g = 0.0f;
-      g = __builtin_fmaf(x[0], ya.x, g);
-      g = __builtin_fmaf(x[1], ya.y, g);
-      g = __builtin_fmaf(x[2], ya.z, g);
-      g = __builtin_fmaf(x[3], ya.w, g);
-      g = __builtin_fmaf(x[4], yb1.x, g);
-      g = __builtin_fmaf(x[5], yb1.y, g);
-      g = __builtin_fmaf(x[6], yb1.z, g);
-      g = __builtin_fmaf(x[7], yb1.w, g);
-      g = __builtin_fmaf(x[8], yc.x, g);
-      g = __builtin_fmaf(x[9], yc.y, g);
-      g = __builtin_fmaf(x[10], yc.z, g);
-      g = __builtin_fmaf(x[11], yc.w, g);
-      gw[kk % kMS] = g;
-      if (kk >= kMS - 1) {
-        const int r = kk - (kMS - 1);
-        // sequential 9-term sum; starting at G_0 instead of 0 + G_0 changes at most the sign of
-        // a zero dot, which (NX - 2 dot) + NY never sees: the keys are bit-identical
-        float dot = gw[r % kMS];
-#pragma unroll
-        for (int u = 1; u < kMS; ++u) dot = dot + gw[(r + u) % kMS];
-        const float d2 = (nqr(r) - 2.0f * dot) + Ns[t + r];
-        const unsigned key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
-        // row-major prefix straight from registers: the 64 lanes write 64 consecutive columns
-        const int col = j0 + t + r;
-        // out-of-range columns (< 0 or >= Np) land in the pad column ldr - 1 (never read):
-        // branchless, no per-row lane masks to keep live
-        if (FAST || r < rows) st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), key >> 16);
-        hrow += ldr;  // next row: one scalar add instead of 32 hoisted row pointers
-        asm volatile("" : "+s"(hrow));
-        // rows past M' in the last strip: kNone in the column plane (no tail mask in the select)
-        tileT[(t + r) * kTP + spos(r)] = (uint16_t)(FAST || r < rows ? key >> 16 : kNone);
-      }
-    }
-    }  // !FAST
-    ACOSS_STAMP(t2);
-    __syncthreads();
-    ACOSS_STAMP(t3);
-    // columns [j0, j0 + 256) complete: column-major prefixes, 32 rows = 64 B per column
-    const int jj = j0 + t;
-#ifdef ACOSS_ABL_NOHC  // timing ablation only (wrong results): no strip-major plane stores
-    if (false) {
-#else
-    if (jj >= 0 && jj < V.Np) {
-#endif
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(tileT + t * kTP);
-      uint4* dh = reinterpret_cast<uint4*>(Hc + ((size_t)strip * ldc + jj) * kSR);  // [strip][column][32 rows]
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint4 h;
-        h.x = src[4 * q];
-        h.y = src[4 * q + 1];
-        h.z = src[4 * q + 2];
-        h.w = src[4 * q + 3];
-        dh[q] = h;
-      }
-    }
-    __syncthreads();
-    // roll the 31-column tail to the front
-    for (int e = t; e < (kSR - 1) * (kTP / 2); e += kSW) {
-      const int c = e / (kTP / 2), w = e - c * (kTP / 2);
-      reinterpret_cast<uint32_t*>(tileT)[c * (kTP / 2) + w] = reinterpret_cast<const uint32_t*>(tileT)[(kSW + c) * (kTP / 2) + w];
-    }
-    ACOSS_STAMP(t4);
-    if (FAST) {
-      ACOSS_STAMP_ADD(0, t0, t1);  // fill + 2 barriers
-      ACOSS_STAMP_ADD(1, t1, t2);  // diagonal walk
-      ACOSS_STAMP_ADD(2, t2, t3);  // barrier after the walk
-      ACOSS_STAMP_ADD(3, t3, t4);  // column-plane stores, barrier, roll
-    }
-  }
-  // kNone over [N', align32(N')) of every row: the row select's last 32-element run then needs
-  // no tail mask. After the barrier, so it lands after the walk's out-of-range stores there.
-  __syncthreads();
-  const int padw = (int)((V.Np + 31) & ~31) - V.Np;
-  for (int e = t; e < kSR * 32; e += kSW) {
-    const int r = e >> 5, c = e & 31;
-    if (c < padw && r < rows) Hr[(size_t)r * ldr + V.Np + c] = (uint16_t)kNone;
-  }
-}
-
 // ---------------------------------------------------------------------------------------
 // Systolic sweep (FAST strips: tau == 1, a full 32-row strip, all 40 query frames in the track).
 // Lane l of a wave holds reference frame jb + l (12 VGPRs) for a whole column block; the
@@ -524,18 +169,20 @@ __device__ __forceinline__ void sweep_body(const PairView& V, int p, int strip, 
 // word order) and a step's row-major prefixes are 56 consecutive columns.
 // ---------------------------------------------------------------------------------------
 constexpr int kSysCols = 56;
-#ifndef ACOSS_SYS_WPE
-#define ACOSS_SYS_WPE 6
-#endif
+constexpr int kThreads = 256;  // sweep block: 4 waves
 
 __device__ __forceinline__ float dpp_shr1(float v) {  // lane l <- lane l - 1 (lane 0 <- 0)
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
 }
 
+// PARTIAL: the last strip of a pair (fewer than 32 rows in the track); the full strips keep a
+// branch-free emit.
+template <bool PARTIAL>
 __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr,
                                                int ldc, int64_t kstride) {
   constexpr int kSteps = kSR + kMS - 1;  // 40
   const int i0 = strip * kSR;
+  const int rows = PARTIAL ? min(kSR, V.Mp - i0) : kSR;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
@@ -614,10 +261,16 @@ __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int str
       if (r >= 0) {
         const f32x2 nq = f32x2{nqr(r), nqr(r + 1)};
         const f32x2 d2 = pk_fma(f32x2{-2.0f, -2.0f}, f32x2{dots[0], dots[1]}, nq) + f32x2{ny, ny};
-        const unsigned k0 = __builtin_bit_cast(unsigned, d2.x > 0.0f ? d2.x : 0.0f);
-        const unsigned k1 = __builtin_bit_cast(unsigned, d2.y > 0.0f ? d2.y : 0.0f);
-        st_u16(hrow, hcol, k0 >> 16);
-        st_u16(hrow, (unsigned)ldr + hcol, k1 >> 16);
+        unsigned k0 = __builtin_bit_cast(unsigned, d2.x > 0.0f ? d2.x : 0.0f);
+        unsigned k1 = __builtin_bit_cast(unsigned, d2.y > 0.0f ? d2.y : 0.0f);
+        if (!PARTIAL || r + 1 < rows) {  // wave-uniform; rows past M' are never stored
+          st_u16(hrow, hcol, k0 >> 16);
+          st_u16(hrow, (unsigned)ldr + hcol, k1 >> 16);
+        } else {
+          if (r < rows) st_u16(hrow, hcol, k0 >> 16);
+          if (r >= rows) k0 = kNone << 16;  // and read as "no element" in the column plane
+          k1 = kNone << 16;
+        }
         hrow += 2 * ldr;
         asm volatile("" : "+s"(hrow));
         if (r < 16) {
@@ -647,227 +300,15 @@ __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int str
 #endif
     }
   }
-  // kNone over [N', align32(N')) of every row (see sweep_body); the walk's stores above went
-  // to valid columns or the pad column only
+  // kNone over [N', align32(N')) of every row: the row select's last 32-element run then needs
+  // no tail mask. After the barrier, so it lands after the walk's stores (which went to valid
+  // columns or the pad column only).
   __syncthreads();
   const int padw = (int)((V.Np + 31) & ~31) - V.Np;
-  for (int e = threadIdx.x; e < kSR * 32; e += kSW) {
+  for (int e = threadIdx.x; e < kSR * 32; e += kThreads) {
     const int r = e >> 5, c = e & 31;
-    if (c < padw) Hr[(size_t)r * ldr + V.Np + c] = (uint16_t)kNone;
+    if (c < padw && r < rows) Hr[(size_t)r * ldr + V.Np + c] = (uint16_t)kNone;
   }
-}
-
-// ---------------------------------------------------------------------------------------
-// MFMA sweep (FAST strips: tau == 1, a full 32-row strip, all 40 query frames in the track).
-// Per panel of kMW diagonals, the Gram terms G(i0 + k, j0 + c) of the panel's parallelogram
-// (0 <= c - k < kMW, k < 40) come from v_mfma_f32_16x16x4f32 tiles: three chained MFMAs over
-// the 12 bins accumulate exactly as the canonical fmaf chain (bins 0..11 from +0), bit for bit
-// (measured on gfx950: profiles/r02/mfma_probe_r02.txt). The tiles land in LDS diagonal-major,
-// Gd[d][k] = G(i0 + k, j0 + d + k); lane d of a wave then walks its diagonal's 16-row half with
-// the 9-term window sums in registers (packed rows r, r + 1, the canonical sequential order),
-// and emits the prefixes exactly as the VALU walk does. The VALU keeps only the window sums and
-// the emits; the LDS carries 4 B per Gram term instead of the 48-B reference frame per term.
-// ---------------------------------------------------------------------------------------
-constexpr int kMW = 128;                  // diagonals per panel
-constexpr int kMCols = kMW + kSR;         // 160 columns touched per panel
-constexpr int kDP = 44;                   // floats per diagonal in Gd (40 used; 44: conflict-free b128 reads)
-constexpr int kMfmaLds = (kMW * kDP + kMCols) * 4 + kMCols * kTP * 2;
-
-typedef float f32x4m __attribute__((ext_vector_type(4)));
-
-// Window sums and emits of rows R0 .. R0 + 15 on diagonal dw (cells (R0 + r, j0 + dw + R0 + r)).
-// EDGE: some columns fall outside [0, N') (first / last panels): their stores go to the pad column.
-template <bool EDGE>
-__device__ __forceinline__ void mfma_walk(const PairView& V, int i0, int j0, int dw, int R0, const float* Gd,
-                                          const float* Ns, uint16_t* tileT, uint16_t* Hr, int ldr) {
-  float g[24];  // G(i0 + R0 + k, j0 + dw + R0 + k), k < 24
-  const f32x4m* src = reinterpret_cast<const f32x4m*>(Gd + dw * kDP + R0);
-#pragma unroll
-  for (int q = 0; q < 6; ++q) {
-    const f32x4m v = src[q];
-    g[4 * q] = v.x;
-    g[4 * q + 1] = v.y;
-    g[4 * q + 2] = v.z;
-    g[4 * q + 3] = v.w;
-  }
-  const float* Nq0 = V.NXq + i0 + R0;
-  auto nqr = [&](int r) {  // row norm: a scalar load at a compile-time offset
-    const float* base = Nq0;
-    asm volatile("" : "+s"(base));
-    return *(const __attribute__((address_space(4))) float*)(base + r);
-  };
-  gu16* hrow = (gu16*)(Hr + (size_t)R0 * ldr);
-  // tileT[(dw + R0 + r) * kTP + spos(R0 + r)], spos(R0 + r) = 2 r + R0 / 16 for r < 16
-  uint16_t* tt = tileT + (dw + R0) * kTP + (R0 >> 4);
-  const int col0 = j0 + dw + R0;
-  const float* ns = Ns + dw + R0;
-#pragma unroll
-  for (int r = 0; r < 16; r += 2) {
-    f32x2 dot = f32x2{g[r], g[r + 1]};
-#pragma unroll
-    for (int u = 1; u < kMS; ++u) dot = dot + f32x2{g[r + u], g[r + u + 1]};
-    const f32x2 nq = f32x2{nqr(r), nqr(r + 1)};
-    const f32x2 ny = f32x2{ns[r], ns[r + 1]};
-    const f32x2 d2 = pk_fma(f32x2{-2.0f, -2.0f}, dot, nq) + ny;  // nq - 2 dot exactly (2 dot is exact)
-    const unsigned k0 = __builtin_bit_cast(unsigned, d2.x > 0.0f ? d2.x : 0.0f);
-    const unsigned k1 = __builtin_bit_cast(unsigned, d2.y > 0.0f ? d2.y : 0.0f);
-    const int col = col0 + r;
-    if (EDGE) {
-      st_u16(hrow, min((unsigned)col, (unsigned)(ldr - 1)), k0 >> 16);
-      st_u16(hrow, ldr + min((unsigned)(col + 1), (unsigned)(ldr - 1)), k1 >> 16);
-    } else {
-      st_u16(hrow, (unsigned)col, k0 >> 16);
-      st_u16(hrow, ldr + (unsigned)(col + 1), k1 >> 16);
-    }
-    hrow += 2 * ldr;
-    asm volatile("" : "+s"(hrow));
-    tt[r * (kTP + 2)] = (uint16_t)(k0 >> 16);
-    tt[(r + 1) * (kTP + 2)] = (uint16_t)(k1 >> 16);
-  }
-}
-
-__device__ __forceinline__ void sweep_body_mfma(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr,
-                                                int ldc, int64_t kstride, float* Gd, float* Ns, uint16_t* tileT) {
-  const int i0 = strip * kSR;
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
-  uint16_t* Hc = K.hc + (size_t)p * kstride;
-  const int li = lane & 15, lk = lane >> 4;
-  // A fragments: query frame i0 + 16 rt + li (rows >= 40 clamped: computed, never stored),
-  // bins 4 s + lk; fixed for the whole strip
-  float a[3][3];
-#pragma unroll
-  for (int rt = 0; rt < 3; ++rt) {
-    const int f = min(i0 + 16 * rt + li, V.nq - 1);
-#pragma unroll
-    for (int s2 = 0; s2 < 3; ++s2) a[rt][s2] = V.X[(size_t)f * 12 + 4 * s2 + lk];
-  }
-  const int dw = 64 * (w & 1) + lane;  // this lane's diagonal in the walk
-  const int R0 = 16 * (w >> 1);        // first row of its half-strip
-  // B fragments of this wave's column tiles ct = w + 4 m (m < 3, ct < 11): reference frame
-  // j0 + 16 ct + li (clamped: out-of-range columns are computed, never stored), bins 4 s + lk.
-  // The next panel's are loaded during this panel's walk.
-  auto load_b = [&](int jn, float (&bf)[3][3]) {
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const int f = min(max(jn + 16 * (w + 4 * m) + li, 0), V.nr - 1);
-      const float* y = V.Yr + (size_t)f * 12 + lk;
-#pragma unroll
-      for (int s2 = 0; s2 < 3; ++s2) bf[m][s2] = y[4 * s2];
-    }
-  };
-  // Gd element of (k, c): (c - k) * kDP + k; this lane's part, c = 16 ct + li, k = 16 rt + 4 lk + i
-  float* gl = Gd + (16 * w + li) * kDP - (kDP - 1) * 4 * lk;
-  const bool k_ok2 = lk < 2;  // row tile 2 holds rows 32..47: only k < 40 is stored
-  float bc[3][3], bn[3][3];
-  load_b(-(kSR - 1), bc);
-  for (int j0 = -(kSR - 1); j0 < V.Np; j0 += kMW) {
-    ACOSS_STAMP(t0);
-    // (the previous panel's walk, copy-out and roll are behind the barriers below)
-    for (int b = t; b < kMCols; b += kSW) {
-      const int jr = j0 + b;
-      Ns[b] = (jr >= 0 && jr < V.Np) ? V.NXr[jr] : 0.0f;
-    }
-    // Gram tiles (rt, ct) with rt <= ct <= rt + 8: three chained MFMAs per tile, the row tiles
-    // of one column tile interleaved so consecutive MFMAs are independent
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const int ct = w + 4 * m;  // wave-uniform
-      if (ct >= 11) continue;
-      const bool v0 = ct <= 8, v1 = ct >= 1 && ct <= 9, v2 = ct >= 2;
-      f32x4m acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = acc0, acc2 = acc0;
-#pragma unroll
-      for (int s2 = 0; s2 < 3; ++s2) {
-        if (v0) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][s2], bc[m][s2], acc0, 0, 0, 0);
-        if (v1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1][s2], bc[m][s2], acc1, 0, 0, 0);
-        if (v2) acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2][s2], bc[m][s2], acc2, 0, 0, 0);
-      }
-      // d = 16 (ct - rt) + li - 4 lk - i: always in [1, 127] for 1 <= ct - rt <= 7; the edge
-      // tiles (ct - rt = 0 or 8) keep d >= 0 / d < kMW per element
-      float* gm = gl + 16 * 4 * m * kDP;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int dl = li - 4 * lk - i;
-        // row tile 0: k = 4 lk + i, d = 16 ct + dl
-        if (v0 && (ct == 0 ? dl >= 0 : (ct == 8 ? dl < 0 : true)))
-          gm[-(kDP - 1) * i] = acc0[i];
-        if (v1 && (ct == 1 ? dl >= 0 : (ct == 9 ? dl < 0 : true)))
-          gm[-16 * kDP + 16 - (kDP - 1) * i] = acc1[i];
-        if (v2 && k_ok2 && (ct == 2 ? dl >= 0 : (ct == 10 ? dl < 0 : true)))
-          gm[-32 * kDP + 32 - (kDP - 1) * i] = acc2[i];
-      }
-    }
-    ACOSS_STAMP(t1);
-    __syncthreads();  // Gd, Ns and the rolled tileT tail are in place
-    ACOSS_STAMP(t2);
-    if (j0 + kMW < V.Np) load_b(j0 + kMW, bn);
-    if (j0 < 0 || j0 + kMCols > V.Np)
-      mfma_walk<true>(V, i0, j0, dw, R0, Gd, Ns, tileT, Hr, ldr);
-    else
-      mfma_walk<false>(V, i0, j0, dw, R0, Gd, Ns, tileT, Hr, ldr);
-#pragma unroll
-    for (int m = 0; m < 3; ++m)
-#pragma unroll
-      for (int s2 = 0; s2 < 3; ++s2) bc[m][s2] = bn[m][s2];
-    ACOSS_STAMP(t3);
-    __syncthreads();
-    // columns [j0, j0 + kMW) complete: strip-major prefixes, 64 B per column
-    if (t < kMW) {
-      const int jj = j0 + t;
-      if (jj >= 0 && jj < V.Np) {
-        const uint32_t* srcw = reinterpret_cast<const uint32_t*>(tileT + t * kTP);
-        uint4* dh = reinterpret_cast<uint4*>(Hc + ((size_t)strip * ldc + jj) * kSR);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) dh[q] = make_uint4(srcw[4 * q], srcw[4 * q + 1], srcw[4 * q + 2], srcw[4 * q + 3]);
-      }
-    }
-    __syncthreads();
-    // roll the 31-column tail to the front (16 used words per column)
-    for (int e = t; e < (kSR - 1) * 16; e += kSW) {
-      const int c2 = e >> 4, w2 = e & 15;
-      reinterpret_cast<uint32_t*>(tileT)[c2 * (kTP / 2) + w2] = reinterpret_cast<const uint32_t*>(tileT)[(kMW + c2) * (kTP / 2) + w2];
-    }
-    ACOSS_STAMP(t4);
-    ACOSS_STAMP_ADD(0, t0, t1);  // norms + Gram tiles
-    ACOSS_STAMP_ADD(1, t1, t2);  // barrier before the walk
-    ACOSS_STAMP_ADD(2, t2, t3);  // walk
-    ACOSS_STAMP_ADD(3, t3, t4);  // barrier, column-plane stores, barrier, roll
-  }
-  // kNone over [N', align32(N')) of every row (see sweep_body)
-  __syncthreads();
-  const int padw = (int)((V.Np + 31) & ~31) - V.Np;
-  for (int e = t; e < kSR * 32; e += kSW) {
-    const int r = e >> 5, c = e & 31;
-    if (c < padw) Hr[(size_t)r * ldr + V.Np + c] = (uint16_t)kNone;
-  }
-}
-
-// edge_only: FAST strips are left to k_sweep_sys9 (unfused systolic path)
-__global__ __launch_bounds__(256) void k_sweep9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride,
-                                                int edge_only) {
-  __shared__ __attribute__((aligned(16))) float Ys[kYsFloats];
-  __shared__ float Ns[kSCols];
-  __shared__ __attribute__((aligned(16))) uint16_t tileT[kSCols * kTP];  // [column][row] 16-bit prefixes
-  const int p = blockIdx.y;
-  const PairView V = pair_view(B, p);
-  const int strip = blockIdx.x, i0 = strip * kSR;
-  if (i0 >= V.Mp || V.Np <= 0) return;
-  if (V.tau == 1 && i0 + kSR <= V.Mp && i0 + kSR + kMS - 1 <= V.nq) {
-    if (!edge_only) sweep_body<true>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
-  } else {
-    sweep_body<false>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
-  }
-}
-
-// Systolic sweep of the FAST strips alone (no LDS): high occupancy while its stores drain.
-__global__ __launch_bounds__(256, ACOSS_SYS_WPE) void k_sweep_sys9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
-                                                                   int64_t kstride) {
-  const int p = blockIdx.y;
-  const PairView V = pair_view(B, p);
-  const int strip = blockIdx.x, i0 = strip * kSR;
-  if (i0 >= V.Mp || V.Np <= 0) return;
-  if (V.tau == 1 && i0 + kSR <= V.Mp && i0 + kSR + kMS - 1 <= V.nq) sweep_body_sys(V, p, strip, K, ldr, ldc, kstride);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1431,7 +872,8 @@ __device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, 
 // k_sel_rows9: one 512-thread block per (32-row strip, pair); wave w takes rows w, w+8, ...
 // Emits T_row and the strip's row-threshold words RT[strip][j] (bit r: key(i0+r, j) <= T_row).
 // ---------------------------------------------------------------------------------------
-constexpr int kRowWaves = 8;
+// LDS of the fused row select: one WaveLds per wave and the strip's row bits
+constexpr int kRowsLds = 4 * (int)sizeof(WaveLds) + kSR * 64 * 4;
 
 // In-register transpose of a 32 x 32 bit matrix: a[r] bit q -> a[q] bit r (stage J swaps the
 // off-diagonal J x J sub-blocks).
@@ -1529,51 +971,23 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
   }
 }
 
-__global__ __launch_bounds__(512, 4) void k_sel_rows9(CrpBatch B, KeyPlanes K, int ldr, int64_t kstride, float kappa,
-                                                   float* __restrict__ thr, float* __restrict__ Tq,
-                                                   int64_t thr_stride, uint32_t* __restrict__ RT,
-                                                   int64_t rt_stride, int ld) {
-  __shared__ WaveLds wl[kRowWaves];
-  __shared__ uint32_t rowbits[kSR][64];
-  const int p = blockIdx.y;
-  const PairView V = pair_view(B, p);
-  const int strip = blockIdx.x;
-  if (strip * kSR >= V.Mp) return;
-  rows_body<kRowWaves>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
-}
 
 // Sweep and row select fused: the block selects the 32 rows it has just swept, reading its
 // full keys back while they are cache-resident (no second pass over F from HBM, one launch
 // fewer). LDS of the two phases is one union.
-constexpr int kSweepLds = (kYsFloats + kSCols) * 4 + kSCols * kTP * 2;
-constexpr int kRowsLds = 4 * (int)sizeof(WaveLds) + kSR * 64 * 4;
-constexpr int kFusedLds0 = kSweepLds > kRowsLds ? kSweepLds : kRowsLds;
-constexpr int kFusedLds = kFusedLds0 > kMfmaLds ? kFusedLds0 : kMfmaLds;
-
-__global__ __launch_bounds__(256, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc, int64_t kstride,
-                                                     float kappa, float* __restrict__ thr, float* __restrict__ Tq,
-                                                     int64_t thr_stride, uint32_t* __restrict__ RT, int64_t rt_stride,
-                                                     int ld, int use_mfma) {
-  __shared__ __attribute__((aligned(16))) char smem[kFusedLds];
-  float* Ys = reinterpret_cast<float*>(smem);
-  float* Ns = Ys + kYsFloats;
-  uint16_t* tileT = reinterpret_cast<uint16_t*>(Ns + kSCols);
+__global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
+                                                          int64_t kstride, float kappa, float* __restrict__ thr,
+                                                          float* __restrict__ Tq, int64_t thr_stride,
+                                                          uint32_t* __restrict__ RT, int64_t rt_stride, int ld) {
+  __shared__ __attribute__((aligned(16))) char smem[kRowsLds];
   const int p = blockIdx.y;
   const PairView V = pair_view(B, p);
   const int strip = blockIdx.x, i0 = strip * kSR;
   if (i0 >= V.Mp || V.Np <= 0) return;
-  if (V.tau == 1 && i0 + kSR <= V.Mp && i0 + kSR + kMS - 1 <= V.nq) {
-    if (use_mfma == 2)
-      sweep_body_sys(V, p, strip, K, ldr, ldc, kstride);
-    else if (use_mfma)
-      sweep_body_mfma(V, p, strip, K, ldr, ldc, kstride, reinterpret_cast<float*>(smem),
-                      reinterpret_cast<float*>(smem) + kMW * kDP,
-                      reinterpret_cast<uint16_t*>(reinterpret_cast<float*>(smem) + kMW * kDP + kMCols));
-    else
-      sweep_body<true>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
-  } else {
-    sweep_body<false>(V, p, strip, K, ldr, ldc, kstride, Ys, Ns, tileT);
-  }
+  if (i0 + kSR <= V.Mp)
+    sweep_body_sys<false>(V, p, strip, K, ldr, ldc, kstride);
+  else
+    sweep_body_sys<true>(V, p, strip, K, ldr, ldc, kstride);
   ACOSS_STAMP(r0);
   __syncthreads();  // the strip's F rows are complete (block-scope visibility of the global stores)
 #ifdef ACOSS_ABL_NOROWS  // timing ablation only (wrong results): sweep without the row select
@@ -1675,46 +1089,18 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
 int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, int ldk, int64_t kstride,
                      uint32_t* RT, float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride,
                      uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s) {
-  if (B.m != kMS || L > 2048) return 1;
+  if (B.m != kMS || B.tau != 1 || L > 2048) return 1;
   const size_t plane = (size_t)nb * kstride;
   const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane};
   const int nstrips = (L + kSR - 1) / kSR;
-  static const bool fused = [] {
-    const char* e = getenv("ACOSS_FUSE_ROWS");
-    return !(e && strcmp(e, "0") == 0);
-  }();
-  // FAST strips: the systolic walk (default), the LDS-fed packed-FP32 diagonal walk
-  // (ACOSS_SWEEP=valu) or the MFMA Gram tiles (ACOSS_SWEEP=mfma); identical keys
-  static const int sweep_mfma = [] {
-    const char* e = getenv("ACOSS_SWEEP");
-    if (e && strcmp(e, "mfma") == 0) return 1;
-    if (e && strcmp(e, "valu") == 0) return 0;
-    return 2;
-  }();
-  if (fused) {
-    prof_begin(PH_SWEEP, s);
-    hipLaunchKernelGGL(k_sweep_rows9, dim3(nstrips, nb), dim3(256), 0, s, B, K, ldk, ldk, kstride, kappa, thr_r, T_r,
-                       thr_stride, RT, mask_stride, ld, sweep_mfma);
-    ACOSS_LAUNCH_CHECK();
-    prof_end(PH_SWEEP, s);
-  } else {
-    prof_begin(PH_SWEEP, s);
-    if (sweep_mfma == 2) {
-      hipLaunchKernelGGL(k_sweep_sys9, dim3(nstrips, nb), dim3(256), 0, s, B, K, ldk, ldk, kstride);
-      ACOSS_LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(k_sweep9, dim3(nstrips, nb), dim3(kSW), 0, s, B, K, ldk, ldk, kstride, sweep_mfma == 2 ? 1 : 0);
-    ACOSS_LAUNCH_CHECK();
-    prof_end(PH_SWEEP, s);
-    prof_begin(PH_SEL_ROWS, s);
-    hipLaunchKernelGGL(k_sel_rows9, dim3(nstrips, nb), dim3(512), 0, s, B, K, ldk, kstride, kappa, thr_r, T_r,
-                       thr_stride, RT, mask_stride, ld);
-    ACOSS_LAUNCH_CHECK();
-    prof_end(PH_SEL_ROWS, s);
-  }
+  prof_begin(PH_SWEEP, s);
+  hipLaunchKernelGGL(k_sweep_rows9, dim3(nstrips, nb), dim3(kThreads), 0, s, B, K, ldk, ldk, kstride, kappa, thr_r,
+                     T_r, thr_stride, RT, mask_stride, ld);
+  ACOSS_LAUNCH_CHECK();
+  prof_end(PH_SWEEP, s);
   prof_begin(PH_SEL_COLS, s);
-  hipLaunchKernelGGL(k_sel_cols9, dim3((L + kColsPerBlock - 1) / kColsPerBlock, nb), dim3(256), 0, s, B, K, ldk, kstride, kappa, RT, thr_c, T_c,
-                     thr_stride, maskT, mask_stride, ld);
+  hipLaunchKernelGGL(k_sel_cols9, dim3((L + kColsPerBlock - 1) / kColsPerBlock, nb), dim3(256), 0, s, B, K, ldk,
+                     kstride, kappa, RT, thr_c, T_c, thr_stride, maskT, mask_stride, ld);
   ACOSS_LAUNCH_CHECK();
   prof_end(PH_SEL_COLS, s);
   return ACOSS_OK;
