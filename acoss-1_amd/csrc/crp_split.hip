@@ -21,6 +21,7 @@
 // were retired in round 2.
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "crp_internal.hpp"
 
@@ -372,6 +373,18 @@ struct Line {
     for (int h = 0; h < KPL / 4; ++h) w8[h] = __builtin_amdgcn_perm(c[h + 8], c[h], 0x06020400u);
   }
   __device__ __forceinline__ bool in_win(unsigned x) const { return win && x >= base8 && x <= base8 + 126u; }
+  // element of mask bit b: lane * KPL + b (ebase() opaque, so element indices are not hoisted
+  // out of callers' loops)
+  __device__ __forceinline__ int ebase() const {
+    int e = (threadIdx.x & 63) * KPL;
+    asm volatile("" : "+v"(e));
+    return e;
+  }
+  __device__ __forceinline__ int elem(int eb, int b) const { return eb + b; }
+  static __device__ __forceinline__ int lane_of(int e) { return e / KPL; }
+  static __device__ __forceinline__ int bit_of(int e) { return e % KPL; }
+  // sample for sample_hint: element KPL * lane (kNone past the line)
+  __device__ __forceinline__ unsigned sample() const { return pv[0] & 0xffffu; }
   __device__ __forceinline__ unsigned pfx(int q) const { return q < 16 ? (pv[q] & 0xffffu) : (pv[q - 16] >> 16); }
   // Lane l's KPL elements start at col0 + l * lane_stride. STORED_SPLIT: the plane holds every
   // run in split order already (the strip-major column plane, written so by the sweep);
@@ -492,6 +505,118 @@ struct Line {
   }
 };
 
+// Short lines (up to 64 KQ elements): lane l holds elements l + 64 q, q < KQ,
+// so a wave-wide ballot of one mask bit is two consecutive 32-element words of the line (the
+// CRP's row and strip words) and every load is coalesced across the wave. KQ/2 packed words:
+// word h = element q = h (bits 0..15) and q = h + KQ/2 (bits 16..31); mask bit h <-> q = h and
+// bit h + 16 <-> q = h + KQ/2, the same flag gather as the long lines' split order. Plain
+// 16-bit search (no window codes: the counts are already KQ/2 words).
+template <int KQ>
+struct LineS {
+  static_assert(KQ == 8 || KQ == 16, "short lines: 8 or 16 elements per lane");
+  unsigned pv[KQ / 2];
+  static __device__ __forceinline__ int q_of_bit(int b) { return b < 16 ? b : b - 16 + KQ / 2; }
+  static __device__ __forceinline__ int bit_of_q(int q) { return q < KQ / 2 ? q : q - KQ / 2 + 16; }
+  __device__ __forceinline__ int ebase() const {
+    int e = threadIdx.x & 63;
+    asm volatile("" : "+v"(e));
+    return e;
+  }
+  __device__ __forceinline__ int elem(int eb, int b) const { return eb + 64 * q_of_bit(b); }
+  static __device__ __forceinline__ int lane_of(int e) { return e & 63; }
+  static __device__ __forceinline__ int bit_of(int e) { return bit_of_q(e >> 6); }
+  __device__ __forceinline__ unsigned pfx(int q) const {
+    return q < KQ / 2 ? (pv[q] & 0xffffu) : (pv[q - KQ / 2] >> 16);
+  }
+  // sample for sample_hint: element l + 64 (l mod KQ), spread over the line
+  __device__ __forceinline__ unsigned sample() const {
+    // a mux tree on the lane bits (an index compare chain becomes a scratch-array lookup)
+    const int lane = threadIdx.x & 63;
+    unsigned t[KQ / 2];
+#pragma unroll
+    for (int k = 0; k < KQ / 2; ++k) t[k] = pv[k];
+#pragma unroll
+    for (int bit = 1, n = KQ / 2; n > 1; bit <<= 1, n >>= 1) {
+      const bool sel = (lane & bit) != 0;
+#pragma unroll
+      for (int k = 0; k < n / 2; ++k) t[k] = sel ? t[2 * k + 1] : t[2 * k];
+    }
+    return (lane & (KQ / 2)) ? (t[0] >> 16) : (t[0] & 0xffffu);
+  }
+  // the n codes of a line; addr(e): where element e's code is. Every lane loads (elements past
+  // the line re-read element n - 1 and are replaced by kNone): no per-element branches.
+  template <class AT>
+  __device__ __forceinline__ void load(AT addr, int n) {
+    const int lane = threadIdx.x & 63;
+    unsigned v[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) v[q] = *addr(min(lane + 64 * q, n - 1));
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) v[q] = lane + 64 * q < n ? v[q] : kNone;
+#pragma unroll
+    for (int h = 0; h < KQ / 2; ++h) pv[h] = v[h] | (v[h + KQ / 2] << 16);
+  }
+  __device__ __forceinline__ int count_le(unsigned x) const {
+    const unsigned X2 = (x + 0x8000u) * 0x10001u;
+    unsigned c = 0;
+#pragma unroll
+    for (int h = 0; h < KQ / 2; ++h) c = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c;
+    return wave_sum((int)c);
+  }
+  __device__ __forceinline__ uint32_t eq_mask(unsigned P) const {
+    const unsigned PP = P * 0x10001u;
+    uint32_t ne = 0;
+#pragma unroll
+    for (int h = 0; h < KQ / 2; ++h) ne = gather_flags(ne, (pv[h] ^ PP) + 0x7fff7fffu, h);
+    return ~ne & kMaskAll;
+  }
+  __device__ __forceinline__ uint32_t le_mask(unsigned x) const {
+    const unsigned X2 = (x + 0x8000u) * 0x10001u;
+    uint32_t le = 0;
+#pragma unroll
+    for (int h = 0; h < KQ / 2; ++h) le = gather_flags(le, X2 - pv[h], h);
+    return le;
+  }
+  static constexpr uint32_t kMaskAll = ((1u << (KQ / 2)) - 1u) * 0x10001u;
+  __device__ __forceinline__ void min_max(unsigned* mn, unsigned* mx) const {
+    unsigned a = 0xffffffffu, b = 0u;
+#pragma unroll
+    for (int h = 0; h < KQ / 2; ++h) {
+      a = pk_min_u16(a, pv[h]);
+      b = pk_max_u16(b, pk_add_u16(pv[h], 0x00010001u) & 0x7fff7fffu);
+    }
+    a = min(a & 0xffffu, a >> 16);
+    b = max(b & 0xffffu, b >> 16);
+    *mn = wave_min_u32(a);
+    const unsigned m = wave_max_u32(b);
+    *mx = m ? m - 1 : 0u;
+  }
+  __device__ __forceinline__ unsigned min_greater(unsigned x) const {
+    unsigned a = 0xffffffffu;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      const unsigned k = pfx(q);
+      a = (k > x && k != kNone) ? min(a, k) : a;
+    }
+    return wave_min_u32(a);
+  }
+};
+
+// Lane t's 32-bit line word t (elements 32 t .. 32 t + 31) from a short line's per-lane mask:
+// word 2q + half is the low / high half of the ballot of bit q. Lanes past 2 KQ get 0.
+template <int KQ>
+__device__ __forceinline__ uint32_t lane_words(uint32_t mask) {
+  const int lane = threadIdx.x & 63;
+  uint32_t out = 0;
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    const unsigned long long bal = __ballot((mask >> LineS<KQ>::bit_of_q(q)) & 1u);
+    const uint32_t w = (lane & 1) ? (uint32_t)(bal >> 32) : (uint32_t)bal;
+    out = (lane >> 1) == q ? w : out;
+  }
+  return out;
+}
+
 // Smallest prefix P with count(keys <= P) > rho, bisecting [a, b]; also returns
 // le = count(<= P) and less = count(< P) (carried through the search: no extra counts).
 // hint (wave-uniform, or kNoHint): the previous line's answer. Adjacent stacked rows/columns
@@ -499,8 +624,8 @@ struct Line {
 // the hint to a bracket, then bisect inside it.
 constexpr unsigned kNoHint = 0xffffffffu;
 
-template <int KPL>
-__device__ __forceinline__ unsigned prefix_of_rank(const Line<KPL>& L, int rho, unsigned a, unsigned b, int n,
+template <class LT>
+__device__ __forceinline__ unsigned prefix_of_rank(const LT& L, int rho, unsigned a, unsigned b, int n,
                                                    unsigned hint, int* le_out, int* less_out, int* passes) {
   int c_b = n;    // count(<= b): every element is <= kmax
   int c_am1 = 0;  // count(<= a - 1): none is below kmin
@@ -551,11 +676,11 @@ struct Hint {
 // quantile in a systematic sample of the line, one element per lane (line elements 32 l),
 // found by repeated wave minima. Off by about ten prefix units, it replaces the [min, max]
 // bisection (about nine counts) by a window search from the guess.
-template <int KPL>
-__device__ __forceinline__ unsigned sample_hint(const Line<KPL>& L, int n, float kappa) {
+template <class LT>
+__device__ __forceinline__ unsigned sample_hint(const LT& L, int n, float kappa) {
   const int lane = threadIdx.x & 63;
-  unsigned v = L.pv[0] & 0xffffu;  // kNone on lanes past the line
-  const int ns = min(64, (n + KPL - 1) / KPL);
+  unsigned v = L.sample();  // kNone on lanes whose sample is past the line
+  const int ns = __popcll(__ballot(v != kNone));
   const int k = (int)((float)(n - 1) * kappa * (float)ns / (float)n);
 #pragma unroll 1
   for (int r = 0; r < k; ++r) {
@@ -583,18 +708,17 @@ struct Group {
   unsigned key;  // its exact key (0xffffffff for lane >= g)
 };
 
-template <int KPL, class KF>
-__device__ Group group_keys(const Line<KPL>& L, unsigned P, int g, const KF& keyf, WaveLds& W) {
+template <class LT, class KF>
+__device__ Group group_keys(const LT& L, unsigned P, int g, const KF& keyf, WaveLds& W) {
   const int lane = threadIdx.x & 63;
-  int ebase = lane * KPL;  // opaque: element indices are not hoisted out of callers' loops
-  asm volatile("" : "+v"(ebase));
+  const int ebase = L.ebase();
   // member list: per-lane SWAR member mask, one wave scan for the lane's first slot, then each
   // lane writes its own members (usually 0-2 per lane; no per-element ballot)
   uint32_t m = L.eq_mask(P);
   const int cnt = __builtin_popcount(m);
   int idx = wave_incl_scan(cnt) - cnt;
   while (m) {
-    W.list[idx++] = ebase + __builtin_ctz(m);
+    W.list[idx++] = L.elem(ebase, __builtin_ctz(m));
     m &= m - 1;
   }
   __builtin_amdgcn_wave_barrier();
@@ -660,19 +784,18 @@ __device__ __forceinline__ void group_rank2(const Group& G, int rho, unsigned* v
 // Members of prefix group P in rounds of 64: round r lists members [64r, 64r + 64) (line order)
 // in W.list and runs fn(element) on lane k < (members in the round). Per-lane member masks and
 // one wave scan give each lane its members' positions; no per-element register arrays.
-template <int KPL, class F>
-__device__ void group_rounds(const Line<KPL>& L, unsigned P, int g, WaveLds& W, F fn) {
+template <class LT, class F>
+__device__ void group_rounds(const LT& L, unsigned P, int g, WaveLds& W, F fn) {
   const int lane = threadIdx.x & 63;
   uint32_t m = L.eq_mask(P);
   const int cnt = __builtin_popcount(m);
   int idx = wave_incl_scan(cnt) - cnt;
-  int ebase = lane * KPL;
-  asm volatile("" : "+v"(ebase));
+  const int ebase = L.ebase();
   for (int r0 = 0; r0 < g; r0 += 64) {
     while (m && idx < r0 + 64) {
       const int q = __builtin_ctz(m);
       m &= m - 1;
-      W.list[idx - r0] = ebase + q;
+      W.list[idx - r0] = L.elem(ebase, q);
       ++idx;
     }
     __builtin_amdgcn_wave_barrier();
@@ -711,8 +834,8 @@ __device__ __forceinline__ unsigned hist_bin_of_rank(const unsigned* hist, int* 
 
 // Key of rank rho in a large prefix group (g > 64; long silences): two passes of recomputed
 // member keys into 8-bit LDS histograms of the low half (bits 15..8, then 7..0).
-template <int KPL, class KF>
-__device__ unsigned big_group_rank(const Line<KPL>& L, unsigned P, int rho, int g, const KF& keyf, WaveLds& W) {
+template <class LT, class KF>
+__device__ unsigned big_group_rank(const LT& L, unsigned P, int rho, int g, const KF& keyf, WaveLds& W) {
   const int lane = threadIdx.x & 63;
   unsigned* hist = reinterpret_cast<unsigned*>(W.gv);  // 256 bins
   unsigned hi8 = 0, lo8 = 0;
@@ -738,8 +861,8 @@ __device__ unsigned big_group_rank(const Line<KPL>& L, unsigned P, int rho, int 
   return (P << 16) | (hi8 << 8) | lo8;
 }
 
-template <int KPL, class KF>
-__device__ unsigned rank_in_prefix(const Line<KPL>& L, unsigned P, int rho, int g, const KF& keyf, WaveLds& W,
+template <class LT, class KF>
+__device__ unsigned rank_in_prefix(const LT& L, unsigned P, int rho, int g, const KF& keyf, WaveLds& W,
                                    Group* cache) {
   if (g <= 64) {
     if (cache->g < 0 || cache->P != P) *cache = group_keys(L, P, g, keyf, W);
@@ -750,8 +873,8 @@ __device__ unsigned rank_in_prefix(const Line<KPL>& L, unsigned P, int rho, int 
 
 // Threshold (distance units) and squared-domain threshold of a line of n keys; leaves the
 // exact keys of the last batched group in *cache for le_bits.
-template <int KPL, class KF>
-__device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF& keyf, WaveLds& W, Group* c_lo,
+template <class LT, class KF>
+__device__ void line_threshold(const LT& L, int n, float kappa, const KF& keyf, WaveLds& W, Group* c_lo,
                                Group* c_hi, float* thr, float* T, Hint* hint) {
   const float q = (float)(n - 1) * kappa;
   const float lo_f = floorf(q), hi_f = ceilf(q);
@@ -829,12 +952,12 @@ __device__ void line_threshold(const Line<KPL>& L, int n, float kappa, const KF&
   ACOSS_STAMP_ADD(KF::kRow ? 38 : 34, ts2, ts3);  // threshold arithmetic
 }
 
-// Bits of "key <= T" for the KPL elements of this lane (element e = lane*KPL + q): every
+// Bits of "key <= T" for this lane's elements (in the line type's bit order): every
 // element whose prefix is <= T's prefix, minus the members of T's prefix group whose exact key
 // exceeds T. The group's exact keys come from the threshold search (the group at the answer's
 // prefix, cached), so normally no member mask or recompute is needed here.
-template <int KPL, class KF>
-__device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, WaveLds& W, const Group& c_lo,
+template <class LT, class KF>
+__device__ uint32_t le_bits(const LT& L, unsigned Tbits, const KF& keyf, WaveLds& W, const Group& c_lo,
                             const Group& c_hi) {
   const unsigned T16 = Tbits >> 16;
   const int lane = threadIdx.x & 63;
@@ -850,17 +973,17 @@ __device__ uint32_t le_bits(const Line<KPL>& L, unsigned Tbits, const KF& keyf, 
     const int cg = lo_hit ? c_lo.g : c_hi.g;
     const unsigned ckey = lo_hit ? c_lo.key : c_hi.key;
     const int celem = lo_hit ? c_lo.elem : c_hi.elem;
-    if (lane < cg && ckey > Tbits) atomicAnd(&W.words[celem / KPL], ~(1u << (celem % KPL)));
+    if (lane < cg && ckey > Tbits) atomicAnd(&W.words[LT::lane_of(celem)], ~(1u << LT::bit_of(celem)));
   } else {
     const int g = wave_sum(__builtin_popcount(L.eq_mask(T16)));
     if (g == 0) return word;
     if (g <= 64) {
       ACOSS_COUNT(KF::kRow ? 10 : 15, 1);
       const Group G = group_keys(L, T16, g, keyf, W);
-      if (lane < G.g && G.key > Tbits) atomicAnd(&W.words[G.elem / KPL], ~(1u << (G.elem % KPL)));
+      if (lane < G.g && G.key > Tbits) atomicAnd(&W.words[LT::lane_of(G.elem)], ~(1u << LT::bit_of(G.elem)));
     } else {  // large group: member keys in rounds of 64
       group_rounds(L, T16, g, W, [&](int e) {
-        if (keyf(e) > Tbits) atomicAnd(&W.words[e / KPL], ~(1u << (e % KPL)));
+        if (keyf(e) > Tbits) atomicAnd(&W.words[LT::lane_of(e)], ~(1u << LT::bit_of(e)));
       });
     }
   }
@@ -899,36 +1022,53 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {
 }
 
 // Row select of one (32-row strip, pair) by NW waves: wave w takes rows w, w+NW, ...
-template <int NW>
+// Line type of a select: KQ = 0 -> the long-line layout (Line<32>), else LineS<KQ>.
+template <int KQ>
+struct LineOf {
+  using T = LineS<KQ>;
+};
+template <>
+struct LineOf<0> {
+  using T = Line<32>;
+};
+
+template <int NW, int KQ>
 __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr,
                                           int64_t kstride, float kappa, float* __restrict__ thr,
                                           float* __restrict__ Tq, int64_t thr_stride, uint32_t* __restrict__ RT,
                                           int64_t rt_stride, int ld, WaveLds* wl, uint32_t (*rowbits)[64]) {
-  constexpr int KPL = 32;
+  using LT = typename LineOf<KQ>::T;
   const int i0 = strip * kSR;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // w: wave-uniform (SGPR)
   WaveLds& W = wl[w];
   constexpr int RPW = kSR / NW;  // consecutive rows per wave: each search starts from its neighbour's
   Hint hint{kNoHint, 1.0f};
   // the next row's line is loaded while this one is searched (its latency hidden)
-  auto load_row = [&](Line<KPL>& Ld, int i) {
+  auto load_row = [&](LT& Ld, int i) {
     int64_t rowoff = (int64_t)p * kstride + (int64_t)i * ldr;
     asm volatile("" : "+s"(rowoff));  // per-row address: nothing per lane hoisted out of the loop
-    Ld.template load_lanes<false>(K.hr + rowoff, KPL, V.Np);
+    if constexpr (KQ == 0) {
+      Ld.template load_lanes<false>(K.hr + rowoff, 32, V.Np);
+    } else {
+      const uint16_t* row = K.hr + rowoff;
+      Ld.load([&](int e) { return row + (unsigned)e; }, V.Np);
+    }
   };
-  Line<KPL> Lnext;
+  LT Lnext;
   if (i0 + w * RPW < V.Mp) load_row(Lnext, i0 + w * RPW);
 #pragma unroll 1
   for (int r = w * RPW; r < (w + 1) * RPW; ++r) {
     const int i = i0 + r;
     uint32_t word = 0;
     if (i < V.Mp) {
-      Line<KPL> L = Lnext;
+      LT L = Lnext;
 #ifndef ACOSS_NO_WINDOW8
 #ifndef ACOSS_NO_SAMPLE_HINT
       if (hint.P == kNoHint) hint.P = sample_hint(L, V.Np, kappa);
 #endif
-      if (hint.P != kNoHint) L.build_window(hint.P);
+      if constexpr (KQ == 0) {
+        if (hint.P != kNoHint) L.build_window(hint.P);
+      }
 #endif
       if (r + 1 < (w + 1) * RPW && i + 1 < V.Mp) load_row(Lnext, i + 1);
       const LineCells<true> keyf{V, i};
@@ -942,6 +1082,7 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
       }
 #ifndef ACOSS_ABL_NOLEBITS
       word = le_bits(L, __builtin_bit_cast(unsigned, T), keyf, W, c_lo, c_hi);
+      if constexpr (KQ != 0) word = lane_words<KQ>(word);  // lane t: columns 32t .. 32t + 31
 #endif
     }
     rowbits[r][lane] = word;
@@ -975,6 +1116,7 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
 // Sweep and row select fused: the block selects the 32 rows it has just swept, reading its
 // full keys back while they are cache-resident (no second pass over F from HBM, one launch
 // fewer). LDS of the two phases is one union.
+template <int KQ>
 __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
                                                           int64_t kstride, float kappa, float* __restrict__ thr,
                                                           float* __restrict__ Tq, int64_t thr_stride,
@@ -993,7 +1135,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
 #ifdef ACOSS_ABL_NOROWS  // timing ablation only (wrong results): sweep without the row select
   return;
 #endif
-  rows_body<4>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld,
+  rows_body<4, KQ>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld,
                reinterpret_cast<WaveLds*>(smem), reinterpret_cast<uint32_t(*)[64]>(smem + 4 * sizeof(WaveLds)));
   ACOSS_STAMP(r1);
   ACOSS_STAMP_ADD(4, r0, r1);  // row select
@@ -1015,11 +1157,13 @@ constexpr int kCPW = ACOSS_CPW;
 #endif
 constexpr int kColsPerBlock = 4 * kCPW;
 
+template <int KQ>
 __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
                                                    const uint32_t* __restrict__ RT, float* __restrict__ thr,
                                                    float* __restrict__ Tq, int64_t thr_stride,
                                                    uint32_t* __restrict__ maskT, int64_t mask_stride, int ld) {
-  constexpr int KPL = 32;
+  constexpr int KPL = 32;  // rows per CRP word (= per lane for long lines)
+  using LT = typename LineOf<KQ>::T;
   __shared__ WaveLds wl[4];
   // neighbouring columns share the lines of RT and the recomputed cells' frames: keep them on one XCD
   const int lb = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
@@ -1031,29 +1175,36 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
   Hint hint{kNoHint, 1.0f};
   const int jend = min(j0 + kCPW, V.Np);
   // the next column's line is loaded while this one is searched (its HBM latency hidden)
-  auto load_col = [&](Line<KPL>& Ld, int j) {
+  auto load_col = [&](LT& Ld, int j) {
     int64_t coloff = (int64_t)p * kstride + (int64_t)j * kSR;
     asm volatile("" : "+s"(coloff));  // per-column address: nothing per lane hoisted out of the loop
-    Ld.template load_lanes<true>(K.hc + coloff, (size_t)ldc * kSR, V.Mp);
+    if constexpr (KQ == 0) {
+      Ld.template load_lanes<true>(K.hc + coloff, (size_t)ldc * kSR, V.Mp);
+    } else {  // row e: strip e / 32, split-order slot of row e % 32 in the strip's 32-row chunk
+      const uint16_t* col = K.hc + coloff;
+      Ld.load([&](int e) { return col + (unsigned)((e >> 5) * ldc * kSR + (e & 15) * 2 + ((e >> 4) & 1)); }, V.Mp);
+    }
   };
 #ifdef ACOSS_COLS_NOPF  // no next-column prefetch: 16 VGPRs fewer (occupancy over latency)
 #pragma unroll 1
   for (int j = j0; j < jend; ++j) {
-    Line<KPL> L;
+    LT L;
     load_col(L, j);
 #else
-  Line<KPL> Lnext;
+  LT Lnext;
   if (j0 < jend) load_col(Lnext, j0);
 #pragma unroll 1
   for (int j = j0; j < jend; ++j) {
-    Line<KPL> L = Lnext;
+    LT L = Lnext;
     if (j + 1 < jend) load_col(Lnext, j + 1);
 #endif
 #ifndef ACOSS_NO_WINDOW8
 #ifndef ACOSS_NO_SAMPLE_HINT
     if (hint.P == kNoHint) hint.P = sample_hint(L, V.Mp, kappa);
 #endif
-    if (hint.P != kNoHint) L.build_window(hint.P);
+    if constexpr (KQ == 0) {
+      if (hint.P != kNoHint) L.build_window(hint.P);
+    }
 #endif
     ACOSS_COUNT(31, 1);  // columns
     // this column's row-threshold word, requested now and used after the select
@@ -1072,7 +1223,8 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
 #ifdef ACOSS_ABL_NOLEBITS
     const uint32_t bits = 0;
 #else
-    const uint32_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
+    uint32_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
+    if constexpr (KQ != 0) bits = lane_words<KQ>(bits);  // lane s: rows 32s .. 32s + 31
 #endif
     if (lane * KPL < V.Mp) maskT[w] = bits & rt;
     ACOSS_STAMP(tc1);
@@ -1093,17 +1245,27 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
   const size_t plane = (size_t)nb * kstride;
   const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane};
   const int nstrips = (L + kSR - 1) / kSR;
-  prof_begin(PH_SWEEP, s);
-  hipLaunchKernelGGL(k_sweep_rows9, dim3(nstrips, nb), dim3(kThreads), 0, s, B, K, ldk, ldk, kstride, kappa, thr_r,
-                     T_r, thr_stride, RT, mask_stride, ld);
-  ACOSS_LAUNCH_CHECK();
-  prof_end(PH_SWEEP, s);
-  prof_begin(PH_SEL_COLS, s);
-  hipLaunchKernelGGL(k_sel_cols9, dim3((L + kColsPerBlock - 1) / kColsPerBlock, nb), dim3(256), 0, s, B, K, ldk,
-                     kstride, kappa, RT, thr_c, T_c, thr_stride, maskT, mask_stride, ld);
-  ACOSS_LAUNCH_CHECK();
-  prof_end(PH_SEL_COLS, s);
-  return ACOSS_OK;
+  // short lines (every line of the batch <= 512 codes) take the lane-strided selects. (16 codes
+  // per lane for lines <= 1024 measured the same as the long-line path, whose window codes
+  // already halve its count words, so only 8 is instantiated.)
+  static const bool no_short = getenv("ACOSS_NO_SHORT") != nullptr;
+  const int kq = no_short ? 0 : (L <= 512 ? 8 : 0);
+  auto launch = [&](auto kqc) -> int {
+    constexpr int KQ = decltype(kqc)::value;
+    prof_begin(PH_SWEEP, s);
+    hipLaunchKernelGGL(k_sweep_rows9<KQ>, dim3(nstrips, nb), dim3(kThreads), 0, s, B, K, ldk, ldk, kstride, kappa,
+                       thr_r, T_r, thr_stride, RT, mask_stride, ld);
+    ACOSS_LAUNCH_CHECK();
+    prof_end(PH_SWEEP, s);
+    prof_begin(PH_SEL_COLS, s);
+    hipLaunchKernelGGL(k_sel_cols9<KQ>, dim3((L + kColsPerBlock - 1) / kColsPerBlock, nb), dim3(256), 0, s, B, K,
+                       ldk, kstride, kappa, RT, thr_c, T_c, thr_stride, maskT, mask_stride, ld);
+    ACOSS_LAUNCH_CHECK();
+    prof_end(PH_SEL_COLS, s);
+    return ACOSS_OK;
+  };
+  if (kq == 8) return launch(std::integral_constant<int, 8>{});
+  return launch(std::integral_constant<int, 0>{});
 }
 
 }  // namespace acoss

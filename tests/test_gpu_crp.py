@@ -141,3 +141,25 @@ def test_crp_align_run_edges():
     np.testing.assert_array_equal(got["oti"].cpu().numpy(), k)
     np.testing.assert_array_equal(got["qmax"].cpu().numpy(), q)
     np.testing.assert_array_equal(got["dmax"].cpu().numpy(), d)
+
+
+@pytest.mark.parametrize("lengths", [[10, 41, 42, 73, 74, 137, 300, 521],   # lines <= 512: lane-strided selects
+                                     [300, 522, 600, 777, 1000, 1033]])  # just past 512: the long-line path
+def test_crp_align_short_lines(lengths):
+    """Lane-strided selects for batches whose lines all fit 512 codes (element l + 64 q on lane
+    l): line ends at every 64-element boundary, a full last lane, silences; and the switch back
+    to the long-line path one code later."""
+    rng = np.random.Generator(np.random.PCG64(sum(lengths)))
+    tracks = []
+    for n in lengths:
+        x = synthetic.render(rng, synthetic.base_sequence(rng, n))
+        if n > 200:
+            x[40:130] = 0.0
+        tracks.append(x)
+    feats, off, lens = synthetic.pack(tracks)
+    pairs = np.array([(i, j) for i in range(len(tracks)) for j in range(len(tracks)) if i != j], np.int32)
+    q, d, k = oracle.crp_batch(feats, off, lens, pairs)
+    got = _lib.crp_align(feats, off, lens, int(lens.max()), pairs, _lib.crp_params(), qmax=True, dmax=True, oti=True)
+    np.testing.assert_array_equal(got["oti"].cpu().numpy(), k)
+    np.testing.assert_array_equal(got["qmax"].cpu().numpy(), q)
+    np.testing.assert_array_equal(got["dmax"].cpu().numpy(), d)
