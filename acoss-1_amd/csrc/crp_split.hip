@@ -1151,11 +1151,17 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
 #ifndef ACOSS_CPW
 #define ACOSS_CPW 2
 #endif
-constexpr int kCPW = ACOSS_CPW;
+// short lines: a run start (sample guess, longer search) is a larger share of a cheap line
+#ifndef ACOSS_CPW_SHORT
+#define ACOSS_CPW_SHORT 4
+#endif
+template <int KQ>
+constexpr int kCPW = KQ ? ACOSS_CPW_SHORT : ACOSS_CPW;
 #ifndef ACOSS_COLS_WPE
 #define ACOSS_COLS_WPE 4
 #endif
-constexpr int kColsPerBlock = 4 * kCPW;
+template <int KQ>
+constexpr int kColsPerBlock = 4 * kCPW<KQ>;
 
 template <int KQ>
 __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
@@ -1169,11 +1175,11 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
   const int lb = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   const int p = lb / gridDim.x;
   const PairView V = pair_view(B, p);
-  const int j0 = (lb - p * gridDim.x) * kColsPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCPW;
+  const int j0 = (lb - p * gridDim.x) * kColsPerBlock<KQ> + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCPW<KQ>;
   WaveLds& W = wl[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
   Hint hint{kNoHint, 1.0f};
-  const int jend = min(j0 + kCPW, V.Np);
+  const int jend = min(j0 + kCPW<KQ>, V.Np);
   // the next column's line is loaded while this one is searched (its HBM latency hidden)
   auto load_col = [&](LT& Ld, int j) {
     int64_t coloff = (int64_t)p * kstride + (int64_t)j * kSR;
@@ -1258,7 +1264,7 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_SWEEP, s);
     prof_begin(PH_SEL_COLS, s);
-    hipLaunchKernelGGL(k_sel_cols9<KQ>, dim3((L + kColsPerBlock - 1) / kColsPerBlock, nb), dim3(256), 0, s, B, K,
+    hipLaunchKernelGGL(k_sel_cols9<KQ>, dim3((L + kColsPerBlock<KQ> - 1) / kColsPerBlock<KQ>, nb), dim3(256), 0, s, B, K,
                        ldk, kstride, kappa, RT, thr_c, T_c, thr_stride, maskT, mask_stride, ld);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_SEL_COLS, s);
