@@ -1116,11 +1116,14 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
 // Sweep and row select fused: the block selects the 32 rows it has just swept, reading its
 // full keys back while they are cache-resident (no second pass over F from HBM, one launch
 // fewer). LDS of the two phases is one union.
+// KQ = 8: every line of the launch is short; KQ = 0: each pair picks its row line type (rows of
+// at most short_n codes take LineS<8>; short_n = 0 disables).
 template <int KQ>
 __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
                                                           int64_t kstride, float kappa, float* __restrict__ thr,
                                                           float* __restrict__ Tq, int64_t thr_stride,
-                                                          uint32_t* __restrict__ RT, int64_t rt_stride, int ld) {
+                                                          uint32_t* __restrict__ RT, int64_t rt_stride, int ld,
+                                                          int short_n) {
   __shared__ __attribute__((aligned(16))) char smem[kRowsLds];
   const int p = blockIdx.y;
   const PairView V = pair_view(B, p);
@@ -1135,8 +1138,12 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
 #ifdef ACOSS_ABL_NOROWS  // timing ablation only (wrong results): sweep without the row select
   return;
 #endif
-  rows_body<4, KQ>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld,
-               reinterpret_cast<WaveLds*>(smem), reinterpret_cast<uint32_t(*)[64]>(smem + 4 * sizeof(WaveLds)));
+  WaveLds* wl = reinterpret_cast<WaveLds*>(smem);
+  uint32_t(*rowbits)[64] = reinterpret_cast<uint32_t(*)[64]>(smem + 4 * sizeof(WaveLds));
+  if (KQ == 8 || V.Np <= short_n)
+    rows_body<4, 8>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+  else
+    rows_body<4, 0>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   ACOSS_STAMP(r1);
   ACOSS_STAMP_ADD(4, r0, r1);  // row select
   if (threadIdx.x == 0) ACOSS_STAMP_ADD(5, 0ull, 1ull);
@@ -1163,23 +1170,16 @@ constexpr int kCPW = KQ ? ACOSS_CPW_SHORT : ACOSS_CPW;
 template <int KQ>
 constexpr int kColsPerBlock = 4 * kCPW<KQ>;
 
+// Columns [j0, jend) of pair p with line type LineOf<KQ>.
 template <int KQ>
-__global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
-                                                   const uint32_t* __restrict__ RT, float* __restrict__ thr,
-                                                   float* __restrict__ Tq, int64_t thr_stride,
-                                                   uint32_t* __restrict__ maskT, int64_t mask_stride, int ld) {
+__device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int jend, const KeyPlanes& K, int ldc,
+                                          int64_t kstride, float kappa, const uint32_t* __restrict__ RT,
+                                          float* __restrict__ thr, float* __restrict__ Tq, int64_t thr_stride,
+                                          uint32_t* __restrict__ maskT, int64_t mask_stride, int ld, WaveLds& W) {
   constexpr int KPL = 32;  // rows per CRP word (= per lane for long lines)
   using LT = typename LineOf<KQ>::T;
-  __shared__ WaveLds wl[4];
-  // neighbouring columns share the lines of RT and the recomputed cells' frames: keep them on one XCD
-  const int lb = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-  const int p = lb / gridDim.x;
-  const PairView V = pair_view(B, p);
-  const int j0 = (lb - p * gridDim.x) * kColsPerBlock<KQ> + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCPW<KQ>;
-  WaveLds& W = wl[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
   Hint hint{kNoHint, 1.0f};
-  const int jend = min(j0 + kCPW<KQ>, V.Np);
   // the next column's line is loaded while this one is searched (its HBM latency hidden)
   auto load_col = [&](LT& Ld, int j) {
     int64_t coloff = (int64_t)p * kstride + (int64_t)j * kSR;
@@ -1238,6 +1238,29 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
   }
 }
 
+
+// KQ = 8: every line of the launch is short (runs of kCPW<8> columns); KQ = 0: runs of kCPW<0>,
+// each pair picking its column line type (columns of at most short_n codes take LineS<8>).
+template <int KQ>
+__global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
+                                                   const uint32_t* __restrict__ RT, float* __restrict__ thr,
+                                                   float* __restrict__ Tq, int64_t thr_stride,
+                                                   uint32_t* __restrict__ maskT, int64_t mask_stride, int ld,
+                                                   int short_n) {
+  __shared__ WaveLds wl[4];
+  // neighbouring columns share the lines of RT and the recomputed cells' frames: keep them on one XCD
+  const int lb = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int p = lb / gridDim.x;
+  const PairView V = pair_view(B, p);
+  const int j0 = (lb - p * gridDim.x) * kColsPerBlock<KQ> + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCPW<KQ>;
+  const int jend = min(j0 + kCPW<KQ>, V.Np);
+  WaveLds& W = wl[threadIdx.x >> 6];
+  if (KQ == 8 || V.Mp <= short_n)
+    cols_body<8>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
+  else
+    cols_body<0>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
+}
+
 }  // namespace
 
 // Three-kernel CRP (m = 9, lines up to 2048 keys). Returns 1 if not applicable.
@@ -1254,18 +1277,20 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
   // short lines (every line of the batch <= 512 codes) take the lane-strided selects. (16 codes
   // per lane for lines <= 1024 measured the same as the long-line path, whose window codes
   // already halve its count words, so only 8 is instantiated.)
+  // mixed batches: each pair picks per side (rows of <= 512 codes, columns of <= 512 codes)
   static const bool no_short = getenv("ACOSS_NO_SHORT") != nullptr;
-  const int kq = no_short ? 0 : (L <= 512 ? 8 : 0);
+  const int short_n = no_short ? 0 : 512;
+  const int kq = (!no_short && L <= 512) ? 8 : 0;
   auto launch = [&](auto kqc) -> int {
     constexpr int KQ = decltype(kqc)::value;
     prof_begin(PH_SWEEP, s);
     hipLaunchKernelGGL(k_sweep_rows9<KQ>, dim3(nstrips, nb), dim3(kThreads), 0, s, B, K, ldk, ldk, kstride, kappa,
-                       thr_r, T_r, thr_stride, RT, mask_stride, ld);
+                       thr_r, T_r, thr_stride, RT, mask_stride, ld, short_n);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_SWEEP, s);
     prof_begin(PH_SEL_COLS, s);
     hipLaunchKernelGGL(k_sel_cols9<KQ>, dim3((L + kColsPerBlock<KQ> - 1) / kColsPerBlock<KQ>, nb), dim3(256), 0, s, B, K,
-                       ldk, kstride, kappa, RT, thr_c, T_c, thr_stride, maskT, mask_stride, ld);
+                       ldk, kstride, kappa, RT, thr_c, T_c, thr_stride, maskT, mask_stride, ld, short_n);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_SEL_COLS, s);
     return ACOSS_OK;
