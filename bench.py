@@ -176,8 +176,9 @@ def main():
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "traffic_latest.json")
         if os.path.exists(tfile):
-            try:
-                traffic = json.load(open(tfile)).get("hbm_bytes_per_launch")
+            try:  # measured on the default workload (profiles/profile.sh): only valid at that length
+                tj = json.load(open(tfile))
+                traffic = tj.get("hbm_bytes_per_launch") if tj.get("frames") == args.frames else None
             except Exception:
                 traffic = None
         kernel_ms_sum = sum(v[0] for v in phases.values()) if phases else None
@@ -204,8 +205,8 @@ def main():
             gq = Dfull[sp[:, 0], sp[:, 1]]
             parity = bool(np.array_equal(gq.astype(np.float32), q))
             cpu = {"value": round(len(sp) / cdt, 3), "unit": "song-pairs/s", "cores": nth, "kind": "port",
-                   "sample": "%d random pairs of the same corpus (2000x2000 frames), oracle/crp_oracle.cpp, "
-                             "%d OpenMP threads, %.1f s" % (len(sp), nth, cdt),
+                   "sample": "%d random pairs of the same corpus (%dx%d frames), oracle/crp_oracle.cpp, "
+                             "%d OpenMP threads, %.1f s" % (len(sp), args.frames, args.frames, nth, cdt),
                    "qmax_bitexact_vs_gpu": parity}
 
         result = {

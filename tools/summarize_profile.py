@@ -37,7 +37,7 @@ for k, v in out.items():
     v["hbm_bytes_corrected"] = hbm
     tot += hbm
 json.dump(out, open(os.path.join(rdir, tag + "_pmc.json"), "w"), indent=1, sort_keys=True)
-json.dump({"source": os.path.join(rdir, tag + "_pmc.json"), "calls": calls,
+json.dump({"source": os.path.join(rdir, tag + "_pmc.json"), "calls": calls, "frames": 2000,  # profile.sh: bench defaults
            "hbm_bytes_per_launch": tot / calls,
            "note": "sum over all acoss kernels of 1024*(2*FETCH_SIZE+WRITE_SIZE) / acoss_crp_align calls"},
           open(os.path.join("profiles", "traffic_latest.json"), "w"), indent=1)
