@@ -1072,7 +1072,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   const int64_t yrot_stride = (int64_t)align_up((size_t)max_len * 12, 64);
   // split path (one sweep + two line-select kernels, crp_split.hip) needs 16-bit key planes
   static const char* path_env = getenv("ACOSS_CRP_PATH");
-  const bool split = m == 9 && tau == 1 && L <= 2048 && !(path_env && strcmp(path_env, "fused") == 0);
+  const bool split = m == 9 && tau == 1 && L <= 4096 && !(path_env && strcmp(path_env, "fused") == 0);
   // row pitch: the selects' 32-element runs end at align32(L); one pad column beyond them takes
   // the sweep's branchless out-of-range stores
   const int ldk = (int)align_up(align_up((size_t)L, 32) + 1, 64);

@@ -427,6 +427,22 @@ struct Line {
   }
   // #elements <= x (x <= 0x7fff): per field (x + 0x8000) - a keeps bit 15 iff a <= x, with no
   // borrow across fields; popcount on VALU, one DPP wave sum (no SGPR per compare, no SALU).
+  // branch-free pieces (window codes / 16-bit words) for Line2, which picks by in_win once for
+  // both halves (the branching forms below are kept for the long lines' own codegen)
+  __device__ __forceinline__ unsigned cnt8(unsigned x) const {
+    const unsigned X4 = (x - base8 + 0x80u) * 0x01010101u;
+    unsigned c = 0;
+#pragma unroll
+    for (int h = 0; h < KPL / 4; ++h) c = __builtin_popcount((X4 - w8[h]) & 0x80808080u) + c;
+    return c;
+  }
+  __device__ __forceinline__ unsigned cnt16(unsigned x) const {
+    const unsigned X2 = (x + 0x8000u) * 0x10001u;
+    unsigned c = 0;
+#pragma unroll
+    for (int h = 0; h < KPL / 2; ++h) c = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c;
+    return c;
+  }
   __device__ __forceinline__ int count_le(unsigned x) const {
     if (in_win(x)) {  // wave-uniform
       const unsigned X4 = (x - base8 + 0x80u) * 0x01010101u;
@@ -436,20 +452,30 @@ struct Line {
       return wave_sum((int)c);
     }
     const unsigned X2 = (x + 0x8000u) * 0x10001u;
-#ifdef ACOSS_CNT_ILP
-    unsigned c[4] = {0, 0, 0, 0};  // four independent v_bcnt chains
-#pragma unroll
-    for (int h = 0; h < KPL / 2; ++h) c[h & 3] = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c[h & 3];
-    return wave_sum((int)((c[0] + c[1]) + (c[2] + c[3])));
-#else
     unsigned c = 0;
 #pragma unroll
     for (int h = 0; h < KPL / 2; ++h) c = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c;
     return wave_sum((int)c);
-#endif
   }
-  // Bit q set iff element q's prefix == P (P <= 0x7f80). Per field, (a ^ P) + 0x7fff keeps bit
+  // Bit q set iff element q's prefix == P (P <= kCodeMax). Per field, (a ^ P) + 0x7fff keeps bit
   // 15 iff a != P; fields are <= 0x7fff, so nothing carries across.
+  __device__ __forceinline__ bool eq_in_win(unsigned P) const {
+    return in_win(P) && (P > base8 || base8 == 0u);  // code 0 is exact only when base8 == 0
+  }
+  __device__ __forceinline__ uint32_t eq8(unsigned P) const {
+    const unsigned PP = (P - base8) * 0x01010101u;
+    uint32_t ne8 = 0;
+#pragma unroll
+    for (int h = 0; h < KPL / 4; ++h) ne8 = gather_flags8(ne8, (w8[h] ^ PP) + 0x7f7f7f7fu, h);
+    return ~ne8;
+  }
+  __device__ __forceinline__ uint32_t eq16(unsigned P) const {
+    const unsigned PP = P * 0x10001u;
+    uint32_t ne = 0;
+#pragma unroll
+    for (int h = 0; h < KPL / 2; ++h) ne = gather_flags(ne, (pv[h] ^ PP) + 0x7fff7fffu, h);
+    return ~ne;
+  }
   __device__ __forceinline__ uint32_t eq_mask(unsigned P) const {
     if (in_win(P) && (P > base8 || base8 == 0u)) {  // code 0 is exact only when base8 == 0
       const unsigned PP = (P - base8) * 0x01010101u;
@@ -465,6 +491,20 @@ struct Line {
     return ~ne;
   }
   // Bit q set iff element q's prefix <= x (x <= 0x7fff; kNone is never <= a real x).
+  __device__ __forceinline__ uint32_t le8(unsigned x) const {
+    const unsigned X4 = (x - base8 + 0x80u) * 0x01010101u;
+    uint32_t le8 = 0;
+#pragma unroll
+    for (int h = 0; h < KPL / 4; ++h) le8 = gather_flags8(le8, X4 - w8[h], h);
+    return le8;
+  }
+  __device__ __forceinline__ uint32_t le16(unsigned x) const {
+    const unsigned X2 = (x + 0x8000u) * 0x10001u;
+    uint32_t le = 0;
+#pragma unroll
+    for (int h = 0; h < KPL / 2; ++h) le = gather_flags(le, X2 - pv[h], h);
+    return le;
+  }
   __device__ __forceinline__ uint32_t le_mask(unsigned x) const {
     if (in_win(x)) {
       const unsigned X4 = (x - base8 + 0x80u) * 0x01010101u;
@@ -480,29 +520,37 @@ struct Line {
     return le;
   }
   // min over elements (kNone is above every real prefix) and max over real elements
-  // (kNone + 1 wraps to 0x8000, masked to 0: below every real prefix + 1)
-  __device__ __forceinline__ void min_max(unsigned* mn, unsigned* mx) const {
-    unsigned a = 0xffffffffu, b = 0u;
+  // (kNone + 1 wraps to 0x8000, masked to 0: below every real prefix + 1); lane shares first
+  __device__ __forceinline__ void min_max_lane(unsigned* a_io, unsigned* b_io) const {
+    unsigned a = *a_io, b = *b_io;
 #pragma unroll
     for (int h = 0; h < KPL / 2; ++h) {
       a = pk_min_u16(a, pv[h]);
       b = pk_max_u16(b, pk_add_u16(pv[h], 0x00010001u) & 0x7fff7fffu);
     }
+    *a_io = a;
+    *b_io = b;
+  }
+  __device__ __forceinline__ void min_max(unsigned* mn, unsigned* mx) const {
+    unsigned a = 0xffffffffu, b = 0u;
+    min_max_lane(&a, &b);
     a = min(a & 0xffffu, a >> 16);
     b = max(b & 0xffffu, b >> 16);
     *mn = wave_min_u32(a);
     const unsigned m = wave_max_u32(b);
     *mx = m ? m - 1 : 0u;
   }
-  __device__ __forceinline__ unsigned min_greater(unsigned x) const {
+  __device__ __forceinline__ unsigned min_greater_lane(unsigned x) const {
     unsigned a = 0xffffffffu;
 #pragma unroll
     for (int q = 0; q < KPL; ++q) {
       const unsigned k = pfx(q);
       a = (k > x && k != kNone) ? min(a, k) : a;
     }
-    return wave_min_u32(a);
+    return a;
   }
+  __device__ __forceinline__ unsigned min_greater(unsigned x) const { return wave_min_u32(min_greater_lane(x)); }
+  static constexpr int kHalves = 1;
 };
 
 // Short lines (up to 64 KQ elements): lane l holds elements l + 64 q, q < KQ,
@@ -578,6 +626,7 @@ struct LineS {
     return le;
   }
   static constexpr uint32_t kMaskAll = ((1u << (KQ / 2)) - 1u) * 0x10001u;
+  static constexpr int kHalves = 1;
   __device__ __forceinline__ void min_max(unsigned* mn, unsigned* mx) const {
     unsigned a = 0xffffffffu, b = 0u;
 #pragma unroll
@@ -616,6 +665,59 @@ __device__ __forceinline__ uint32_t lane_words(uint32_t mask) {
   }
   return out;
 }
+
+// Lines of 2049..4096 codes: two long-line halves held by one wave, elements [0, 2048) in A
+// and [2048, n) in B (lane l: elements 32 l.. and 2048 + 32 l..). One wave sum per count; masks
+// are 64-bit (A in bits 0..31, B in 32..63); the le words of B live in W.words[64 + lane].
+struct Line2 {
+  Line<32> A, B;
+  static constexpr int kHalves = 2;
+  __device__ __forceinline__ int ebase() const { return A.ebase(); }
+  __device__ __forceinline__ int elem(int eb, int b) const { return b < 32 ? eb + b : 2048 + eb + (b - 32); }
+  static __device__ __forceinline__ int lane_of(int e) { return e < 2048 ? (e >> 5) : 64 + ((e - 2048) >> 5); }
+  static __device__ __forceinline__ int bit_of(int e) { return e & 31; }
+  // sample: even lanes from A (element 32 l), odd lanes from B (element 2048 + 32 l)
+  __device__ __forceinline__ unsigned sample() const {
+    const unsigned a = A.sample(), b = B.sample();  // (selecting the half object would keep both in scratch)
+    return (threadIdx.x & 1) ? b : a;
+  }
+  __device__ __forceinline__ void build_window(unsigned c) {
+    A.build_window(c);
+    B.build_window(c);
+  }
+  // (both halves share the window, so one wave-uniform branch serves both: branching per half
+  // lets the compiler merge the two halves' paths into pointer phis, which keeps the line in scratch)
+  __device__ __forceinline__ int count_le(unsigned x) const {
+    if (A.in_win(x)) return wave_sum((int)(A.cnt8(x) + B.cnt8(x)));
+    return wave_sum((int)(A.cnt16(x) + B.cnt16(x)));
+  }
+  __device__ __forceinline__ uint64_t eq_mask(unsigned P) const {
+    if (A.eq_in_win(P)) return (uint64_t)A.eq8(P) | ((uint64_t)B.eq8(P) << 32);
+    return (uint64_t)A.eq16(P) | ((uint64_t)B.eq16(P) << 32);
+  }
+  __device__ __forceinline__ uint64_t le_mask(unsigned x) const {
+    if (A.in_win(x)) return (uint64_t)A.le8(x) | ((uint64_t)B.le8(x) << 32);
+    return (uint64_t)A.le16(x) | ((uint64_t)B.le16(x) << 32);
+  }
+  __device__ __forceinline__ void min_max(unsigned* mn, unsigned* mx) const {
+    unsigned a = 0xffffffffu, b = 0u;
+    A.min_max_lane(&a, &b);
+    B.min_max_lane(&a, &b);
+    a = min(a & 0xffffu, a >> 16);
+    b = max(b & 0xffffu, b >> 16);
+    *mn = wave_min_u32(a);
+    const unsigned m = wave_max_u32(b);
+    *mx = m ? m - 1 : 0u;
+  }
+  __device__ __forceinline__ unsigned min_greater(unsigned x) const {
+    return wave_min_u32(min(A.min_greater_lane(x), B.min_greater_lane(x)));
+  }
+};
+
+__device__ __forceinline__ int popc(uint32_t m) { return __builtin_popcount(m); }
+__device__ __forceinline__ int popc(uint64_t m) { return __builtin_popcountll(m); }
+__device__ __forceinline__ int ctz(uint32_t m) { return __builtin_ctz(m); }
+__device__ __forceinline__ int ctz(uint64_t m) { return __builtin_ctzll(m); }
 
 // Smallest prefix P with count(keys <= P) > rho, bisecting [a, b]; also returns
 // le = count(<= P) and less = count(< P) (carried through the search: no extra counts).
@@ -695,7 +797,7 @@ __device__ __forceinline__ unsigned sample_hint(const LT& L, int n, float kappa)
 // Scratch of one wave in LDS: element list and 64 bit-words.
 struct WaveLds {
   int list[64];
-  uint32_t words[64];
+  uint32_t words[128];  // le words (64 per line half)
   float gv[64 * kMS];  // Gram terms of a group's cells, [member][frame]
 };
 
@@ -709,16 +811,16 @@ struct Group {
 };
 
 template <class LT, class KF>
-__device__ Group group_keys(const LT& L, unsigned P, int g, const KF& keyf, WaveLds& W) {
+__device__ __forceinline__ Group group_keys(const LT& L, unsigned P, int g, const KF& keyf, WaveLds& W) {
   const int lane = threadIdx.x & 63;
   const int ebase = L.ebase();
   // member list: per-lane SWAR member mask, one wave scan for the lane's first slot, then each
   // lane writes its own members (usually 0-2 per lane; no per-element ballot)
-  uint32_t m = L.eq_mask(P);
-  const int cnt = __builtin_popcount(m);
+  auto m = L.eq_mask(P);
+  const int cnt = popc(m);
   int idx = wave_incl_scan(cnt) - cnt;
   while (m) {
-    W.list[idx++] = L.elem(ebase, __builtin_ctz(m));
+    W.list[idx++] = L.elem(ebase, ctz(m));
     m &= m - 1;
   }
   __builtin_amdgcn_wave_barrier();
@@ -785,15 +887,15 @@ __device__ __forceinline__ void group_rank2(const Group& G, int rho, unsigned* v
 // in W.list and runs fn(element) on lane k < (members in the round). Per-lane member masks and
 // one wave scan give each lane its members' positions; no per-element register arrays.
 template <class LT, class F>
-__device__ void group_rounds(const LT& L, unsigned P, int g, WaveLds& W, F fn) {
+__device__ __forceinline__ void group_rounds(const LT& L, unsigned P, int g, WaveLds& W, F fn) {
   const int lane = threadIdx.x & 63;
-  uint32_t m = L.eq_mask(P);
-  const int cnt = __builtin_popcount(m);
+  auto m = L.eq_mask(P);
+  const int cnt = popc(m);
   int idx = wave_incl_scan(cnt) - cnt;
   const int ebase = L.ebase();
   for (int r0 = 0; r0 < g; r0 += 64) {
     while (m && idx < r0 + 64) {
-      const int q = __builtin_ctz(m);
+      const int q = ctz(m);
       m &= m - 1;
       W.list[idx - r0] = L.elem(ebase, q);
       ++idx;
@@ -835,7 +937,7 @@ __device__ __forceinline__ unsigned hist_bin_of_rank(const unsigned* hist, int* 
 // Key of rank rho in a large prefix group (g > 64; long silences): two passes of recomputed
 // member keys into 8-bit LDS histograms of the low half (bits 15..8, then 7..0).
 template <class LT, class KF>
-__device__ unsigned big_group_rank(const LT& L, unsigned P, int rho, int g, const KF& keyf, WaveLds& W) {
+__device__ __forceinline__ unsigned big_group_rank(const LT& L, unsigned P, int rho, int g, const KF& keyf, WaveLds& W) {
   const int lane = threadIdx.x & 63;
   unsigned* hist = reinterpret_cast<unsigned*>(W.gv);  // 256 bins
   unsigned hi8 = 0, lo8 = 0;
@@ -862,7 +964,7 @@ __device__ unsigned big_group_rank(const LT& L, unsigned P, int rho, int g, cons
 }
 
 template <class LT, class KF>
-__device__ unsigned rank_in_prefix(const LT& L, unsigned P, int rho, int g, const KF& keyf, WaveLds& W,
+__device__ __forceinline__ unsigned rank_in_prefix(const LT& L, unsigned P, int rho, int g, const KF& keyf, WaveLds& W,
                                    Group* cache) {
   if (g <= 64) {
     if (cache->g < 0 || cache->P != P) *cache = group_keys(L, P, g, keyf, W);
@@ -874,7 +976,7 @@ __device__ unsigned rank_in_prefix(const LT& L, unsigned P, int rho, int g, cons
 // Threshold (distance units) and squared-domain threshold of a line of n keys; leaves the
 // exact keys of the last batched group in *cache for le_bits.
 template <class LT, class KF>
-__device__ void line_threshold(const LT& L, int n, float kappa, const KF& keyf, WaveLds& W, Group* c_lo,
+__device__ __forceinline__ void line_threshold(const LT& L, int n, float kappa, const KF& keyf, WaveLds& W, Group* c_lo,
                                Group* c_hi, float* thr, float* T, Hint* hint) {
   const float q = (float)(n - 1) * kappa;
   const float lo_f = floorf(q), hi_f = ceilf(q);
@@ -957,17 +1059,18 @@ __device__ void line_threshold(const LT& L, int n, float kappa, const KF& keyf, 
 // exceeds T. The group's exact keys come from the threshold search (the group at the answer's
 // prefix, cached), so normally no member mask or recompute is needed here.
 template <class LT, class KF>
-__device__ uint32_t le_bits(const LT& L, unsigned Tbits, const KF& keyf, WaveLds& W, const Group& c_lo,
+__device__ __forceinline__ auto le_bits(const LT& L, unsigned Tbits, const KF& keyf, WaveLds& W, const Group& c_lo,
                             const Group& c_hi) {
   const unsigned T16 = Tbits >> 16;
   const int lane = threadIdx.x & 63;
-  const uint32_t word = L.le_mask(T16);  // kNone is never <= T16 <= 0x7f80
+  const auto word = L.le_mask(T16);  // kNone is never <= T16 <= 0x7f80
 #ifdef ACOSS_ABL_NOGROUP2  // timing ablation only (wrong results): prefix-only decision
   return word;
 #endif
   // (selected by value: a pointer to either cached group would put both on the stack)
   const bool lo_hit = c_lo.g >= 0 && c_lo.P == T16, hi_hit = c_hi.g >= 0 && c_hi.P == T16;
   W.words[lane] = 0xffffffffu;
+  if (LT::kHalves == 2) W.words[64 + lane] = 0xffffffffu;
   __builtin_amdgcn_wave_barrier();
   if (lo_hit || hi_hit) {
     const int cg = lo_hit ? c_lo.g : c_hi.g;
@@ -975,7 +1078,7 @@ __device__ uint32_t le_bits(const LT& L, unsigned Tbits, const KF& keyf, WaveLds
     const int celem = lo_hit ? c_lo.elem : c_hi.elem;
     if (lane < cg && ckey > Tbits) atomicAnd(&W.words[LT::lane_of(celem)], ~(1u << LT::bit_of(celem)));
   } else {
-    const int g = wave_sum(__builtin_popcount(L.eq_mask(T16)));
+    const int g = wave_sum(popc(L.eq_mask(T16)));
     if (g == 0) return word;
     if (g <= 64) {
       ACOSS_COUNT(KF::kRow ? 10 : 15, 1);
@@ -988,7 +1091,10 @@ __device__ uint32_t le_bits(const LT& L, unsigned Tbits, const KF& keyf, WaveLds
     }
   }
   __builtin_amdgcn_wave_barrier();
-  return word & W.words[lane];
+  if constexpr (LT::kHalves == 2)
+    return word & (((uint64_t)W.words[64 + lane] << 32) | W.words[lane]);
+  else
+    return word & W.words[lane];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -997,6 +1103,8 @@ __device__ uint32_t le_bits(const LT& L, unsigned Tbits, const KF& keyf, WaveLds
 // ---------------------------------------------------------------------------------------
 // LDS of the fused row select: one WaveLds per wave and the strip's row bits
 constexpr int kRowsLds = 4 * (int)sizeof(WaveLds) + kSR * 64 * 4;
+// launches with lines past 2048 codes: row bits of 128 words per row
+constexpr int kRowsLds2 = 4 * (int)sizeof(WaveLds) + kSR * 128 * 4;
 
 // In-register transpose of a 32 x 32 bit matrix: a[r] bit q -> a[q] bit r (stage J swaps the
 // off-diagonal J x J sub-blocks).
@@ -1031,12 +1139,16 @@ template <>
 struct LineOf<0> {
   using T = Line<32>;
 };
+template <>
+struct LineOf<2> {
+  using T = Line2;
+};
 
-template <int NW, int KQ>
+template <int NW, int KQ, int RB>
 __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr,
                                           int64_t kstride, float kappa, float* __restrict__ thr,
                                           float* __restrict__ Tq, int64_t thr_stride, uint32_t* __restrict__ RT,
-                                          int64_t rt_stride, int ld, WaveLds* wl, uint32_t (*rowbits)[64]) {
+                                          int64_t rt_stride, int ld, WaveLds* wl, uint32_t (*rowbits)[RB]) {
   using LT = typename LineOf<KQ>::T;
   const int i0 = strip * kSR;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // w: wave-uniform (SGPR)
@@ -1049,6 +1161,9 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
     asm volatile("" : "+s"(rowoff));  // per-row address: nothing per lane hoisted out of the loop
     if constexpr (KQ == 0) {
       Ld.template load_lanes<false>(K.hr + rowoff, 32, V.Np);
+    } else if constexpr (KQ == 2) {
+      Ld.A.template load_lanes<false>(K.hr + rowoff, 32, V.Np);
+      Ld.B.template load_lanes<false>(K.hr + rowoff + 2048, 32, V.Np - 2048);
     } else {
       const uint16_t* row = K.hr + rowoff;
       Ld.load([&](int e) { return row + (unsigned)e; }, V.Np);
@@ -1059,14 +1174,14 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
 #pragma unroll 1
   for (int r = w * RPW; r < (w + 1) * RPW; ++r) {
     const int i = i0 + r;
-    uint32_t word = 0;
+    uint64_t word = 0;  // (Line2: the second half's word in bits 32..63)
     if (i < V.Mp) {
       LT L = Lnext;
 #ifndef ACOSS_NO_WINDOW8
 #ifndef ACOSS_NO_SAMPLE_HINT
       if (hint.P == kNoHint) hint.P = sample_hint(L, V.Np, kappa);
 #endif
-      if constexpr (KQ == 0) {
+      if constexpr (KQ == 0 || KQ == 2) {
         if (hint.P != kNoHint) L.build_window(hint.P);
       }
 #endif
@@ -1082,10 +1197,11 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
       }
 #ifndef ACOSS_ABL_NOLEBITS
       word = le_bits(L, __builtin_bit_cast(unsigned, T), keyf, W, c_lo, c_hi);
-      if constexpr (KQ != 0) word = lane_words<KQ>(word);  // lane t: columns 32t .. 32t + 31
+      if constexpr (KQ == 8) word = lane_words<KQ>((uint32_t)word);  // lane t: columns 32t .. 32t + 31
 #endif
     }
-    rowbits[r][lane] = word;
+    rowbits[r][lane] = (uint32_t)word;
+    if constexpr (KQ == 2) rowbits[r][64 + lane] = (uint32_t)(word >> 32);
   }
   __syncthreads();
   // transpose: word of column j = bit (j & 31) of rowbits[r][j >> 5], r = 0..31. Thread b takes
@@ -1117,14 +1233,16 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
 // full keys back while they are cache-resident (no second pass over F from HBM, one launch
 // fewer). LDS of the two phases is one union.
 // KQ = 8: every line of the launch is short; KQ = 0: each pair picks its row line type (rows of
-// at most short_n codes take LineS<8>; short_n = 0 disables).
+// at most short_n codes take LineS<8>; short_n = 0 disables); KQ = 2: as 0, and rows past 2048
+// codes take Line2.
 template <int KQ>
-__global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
+__global__ __launch_bounds__(kThreads, KQ == 2 ? 3 : 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
                                                           int64_t kstride, float kappa, float* __restrict__ thr,
                                                           float* __restrict__ Tq, int64_t thr_stride,
                                                           uint32_t* __restrict__ RT, int64_t rt_stride, int ld,
                                                           int short_n) {
-  __shared__ __attribute__((aligned(16))) char smem[kRowsLds];
+  constexpr int RB = KQ == 2 ? 128 : 64;  // row-bit words per row
+  __shared__ __attribute__((aligned(16))) char smem[KQ == 2 ? kRowsLds2 : kRowsLds];
   const int p = blockIdx.y;
   const PairView V = pair_view(B, p);
   const int strip = blockIdx.x, i0 = strip * kSR;
@@ -1139,11 +1257,13 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
   return;
 #endif
   WaveLds* wl = reinterpret_cast<WaveLds*>(smem);
-  uint32_t(*rowbits)[64] = reinterpret_cast<uint32_t(*)[64]>(smem + 4 * sizeof(WaveLds));
+  uint32_t(*rowbits)[RB] = reinterpret_cast<uint32_t(*)[RB]>(smem + 4 * sizeof(WaveLds));
   if (KQ == 8 || V.Np <= short_n)
-    rows_body<4, 8>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+    rows_body<4, 8, RB>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+  else if (KQ == 2 && V.Np > 2048)
+    rows_body<4, 2, RB>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   else
-    rows_body<4, 0>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+    rows_body<4, 0, RB>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   ACOSS_STAMP(r1);
   ACOSS_STAMP_ADD(4, r0, r1);  // row select
   if (threadIdx.x == 0) ACOSS_STAMP_ADD(5, 0ull, 1ull);
@@ -1163,7 +1283,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
 #define ACOSS_CPW_SHORT 4
 #endif
 template <int KQ>
-constexpr int kCPW = KQ ? ACOSS_CPW_SHORT : ACOSS_CPW;
+constexpr int kCPW = KQ == 8 ? ACOSS_CPW_SHORT : ACOSS_CPW;
 #ifndef ACOSS_COLS_WPE
 #define ACOSS_COLS_WPE 4
 #endif
@@ -1186,6 +1306,9 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
     asm volatile("" : "+s"(coloff));  // per-column address: nothing per lane hoisted out of the loop
     if constexpr (KQ == 0) {
       Ld.template load_lanes<true>(K.hc + coloff, (size_t)ldc * kSR, V.Mp);
+    } else if constexpr (KQ == 2) {  // rows 2048.. start at strip 64
+      Ld.A.template load_lanes<true>(K.hc + coloff, (size_t)ldc * kSR, V.Mp);
+      Ld.B.template load_lanes<true>(K.hc + coloff + (size_t)64 * ldc * kSR, (size_t)ldc * kSR, V.Mp - 2048);
     } else {  // row e: strip e / 32, split-order slot of row e % 32 in the strip's 32-row chunk
       const uint16_t* col = K.hc + coloff;
       Ld.load([&](int e) { return col + (unsigned)((e >> 5) * ldc * kSR + (e & 15) * 2 + ((e >> 4) & 1)); }, V.Mp);
@@ -1208,7 +1331,7 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
 #ifndef ACOSS_NO_SAMPLE_HINT
     if (hint.P == kNoHint) hint.P = sample_hint(L, V.Mp, kappa);
 #endif
-    if constexpr (KQ == 0) {
+    if constexpr (KQ == 0 || KQ == 2) {
       if (hint.P != kNoHint) L.build_window(hint.P);
     }
 #endif
@@ -1216,6 +1339,9 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
     // this column's row-threshold word, requested now and used after the select
     const size_t w = (size_t)p * mask_stride + (size_t)(lane * KPL < V.Mp ? lane : 0) * ld + j;
     const uint32_t rt = RT[w];
+    // Line2: the second half's strip 64 + lane
+    const size_t w2 = (size_t)p * mask_stride + (size_t)(2048 + lane * KPL < V.Mp ? 64 + lane : 0) * ld + j;
+    const uint32_t rt2 = KQ == 2 ? RT[w2] : 0u;
     const LineCells<false> keyf{V, j};
     float th, Tc;
     Group c_lo, c_hi;
@@ -1227,12 +1353,13 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
     }
     ACOSS_STAMP(tc0);
 #ifdef ACOSS_ABL_NOLEBITS
-    const uint32_t bits = 0;
+    const uint64_t bits = 0;
 #else
-    uint32_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
-    if constexpr (KQ != 0) bits = lane_words<KQ>(bits);  // lane s: rows 32s .. 32s + 31
+    uint64_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
+    if constexpr (KQ == 8) bits = lane_words<KQ>((uint32_t)bits);  // lane s: rows 32s .. 32s + 31
 #endif
-    if (lane * KPL < V.Mp) maskT[w] = bits & rt;
+    if (lane * KPL < V.Mp) maskT[w] = (uint32_t)bits & rt;
+    if (KQ == 2 && 2048 + lane * KPL < V.Mp) maskT[w2] = (uint32_t)(bits >> 32) & rt2;
     ACOSS_STAMP(tc1);
     ACOSS_STAMP_ADD(35, tc0, tc1);  // le_bits and the CRP word
   }
@@ -1240,9 +1367,10 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
 
 
 // KQ = 8: every line of the launch is short (runs of kCPW<8> columns); KQ = 0: runs of kCPW<0>,
-// each pair picking its column line type (columns of at most short_n codes take LineS<8>).
+// each pair picking its column line type (columns of at most short_n codes take LineS<8>);
+// KQ = 2: as 0, and columns past 2048 codes take Line2.
 template <int KQ>
-__global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
+__global__ __launch_bounds__(256, KQ == 2 ? 3 : ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
                                                    const uint32_t* __restrict__ RT, float* __restrict__ thr,
                                                    float* __restrict__ Tq, int64_t thr_stride,
                                                    uint32_t* __restrict__ maskT, int64_t mask_stride, int ld,
@@ -1257,20 +1385,22 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
   WaveLds& W = wl[threadIdx.x >> 6];
   if (KQ == 8 || V.Mp <= short_n)
     cols_body<8>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
+  else if (KQ == 2 && V.Mp > 2048)
+    cols_body<2>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
   else
     cols_body<0>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
 }
 
 }  // namespace
 
-// Three-kernel CRP (m = 9, lines up to 2048 keys). Returns 1 if not applicable.
+// Two-kernel CRP (m = 9, tau = 1, lines up to 4096 keys). Returns 1 if not applicable.
 // kplanes: nb * kstride uint16 row-major prefixes, then nb * kstride uint16 strip-major ones;
 // RT: nb * mask_stride
 // words (same layout as maskT).
 int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, int ldk, int64_t kstride,
                      uint32_t* RT, float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride,
                      uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s) {
-  if (B.m != kMS || B.tau != 1 || L > 2048) return 1;
+  if (B.m != kMS || B.tau != 1 || L > 4096) return 1;
   const size_t plane = (size_t)nb * kstride;
   const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane};
   const int nstrips = (L + kSR - 1) / kSR;
@@ -1280,7 +1410,7 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
   // mixed batches: each pair picks per side (rows of <= 512 codes, columns of <= 512 codes)
   static const bool no_short = getenv("ACOSS_NO_SHORT") != nullptr;
   const int short_n = no_short ? 0 : 512;
-  const int kq = (!no_short && L <= 512) ? 8 : 0;
+  const int kq = L > 2048 ? 2 : ((!no_short && L <= 512) ? 8 : 0);  // 2: some line past 2048
   auto launch = [&](auto kqc) -> int {
     constexpr int KQ = decltype(kqc)::value;
     prof_begin(PH_SWEEP, s);
@@ -1296,6 +1426,7 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
     return ACOSS_OK;
   };
   if (kq == 8) return launch(std::integral_constant<int, 8>{});
+  if (kq == 2) return launch(std::integral_constant<int, 2>{});
   return launch(std::integral_constant<int, 0>{});
 }
 

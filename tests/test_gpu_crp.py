@@ -163,3 +163,22 @@ def test_crp_align_short_lines(lengths):
     np.testing.assert_array_equal(got["oti"].cpu().numpy(), k)
     np.testing.assert_array_equal(got["qmax"].cpu().numpy(), q)
     np.testing.assert_array_equal(got["dmax"].cpu().numpy(), d)
+
+
+def test_crp_align_long_lines():
+    """Lines of 2049..4096 codes (tracks of 2058..4105 frames) stay on the split path: one wave
+    holds both 2048-code halves of a line (Line2), mixed in one launch with shorter lines."""
+    rng = np.random.Generator(np.random.PCG64(11))
+    tracks = []
+    for n in [300, 2057, 2058, 2600, 4105]:
+        x = synthetic.render(rng, synthetic.base_sequence(rng, n))
+        if n > 2000:
+            x[1900:2300] = 0.0  # a silence across the halves' boundary
+        tracks.append(x)
+    feats, off, lens = synthetic.pack(tracks)
+    pairs = np.array([(i, j) for i in range(len(tracks)) for j in range(len(tracks)) if i != j], np.int32)
+    q, d, k = oracle.crp_batch(feats, off, lens, pairs)
+    got = _lib.crp_align(feats, off, lens, int(lens.max()), pairs, _lib.crp_params(), qmax=True, dmax=True, oti=True)
+    np.testing.assert_array_equal(got["oti"].cpu().numpy(), k)
+    np.testing.assert_array_equal(got["qmax"].cpu().numpy(), q)
+    np.testing.assert_array_equal(got["dmax"].cpu().numpy(), d)
