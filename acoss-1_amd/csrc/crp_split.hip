@@ -1169,14 +1169,20 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
       Ld.load([&](int e) { return row + (unsigned)e; }, V.Np);
     }
   };
+  // Line2 loads each line when it starts (no prefetch: 48 VGPRs, the 4th wave per SIMD)
+  constexpr bool kPF = KQ != 2;
   LT Lnext;
-  if (i0 + w * RPW < V.Mp) load_row(Lnext, i0 + w * RPW);
+  if (kPF && i0 + w * RPW < V.Mp) load_row(Lnext, i0 + w * RPW);
 #pragma unroll 1
   for (int r = w * RPW; r < (w + 1) * RPW; ++r) {
     const int i = i0 + r;
     uint64_t word = 0;  // (Line2: the second half's word in bits 32..63)
     if (i < V.Mp) {
-      LT L = Lnext;
+      LT L;
+      if constexpr (kPF)
+        L = Lnext;
+      else
+        load_row(L, i);
 #ifndef ACOSS_NO_WINDOW8
 #ifndef ACOSS_NO_SAMPLE_HINT
       if (hint.P == kNoHint) hint.P = sample_hint(L, V.Np, kappa);
@@ -1185,7 +1191,7 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
         if (hint.P != kNoHint) L.build_window(hint.P);
       }
 #endif
-      if (r + 1 < (w + 1) * RPW && i + 1 < V.Mp) load_row(Lnext, i + 1);
+      if (kPF && r + 1 < (w + 1) * RPW && i + 1 < V.Mp) load_row(Lnext, i + 1);
       const LineCells<true> keyf{V, i};
       float th, T;
       Group c_lo, c_hi;
@@ -1236,7 +1242,7 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
 // at most short_n codes take LineS<8>; short_n = 0 disables); KQ = 2: as 0, and rows past 2048
 // codes take Line2.
 template <int KQ>
-__global__ __launch_bounds__(kThreads, KQ == 2 ? 3 : 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
+__global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
                                                           int64_t kstride, float kappa, float* __restrict__ thr,
                                                           float* __restrict__ Tq, int64_t thr_stride,
                                                           uint32_t* __restrict__ RT, int64_t rt_stride, int ld,
@@ -1320,12 +1326,17 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
     LT L;
     load_col(L, j);
 #else
+  constexpr bool kPF = KQ != 2;  // as the rows
   LT Lnext;
-  if (j0 < jend) load_col(Lnext, j0);
+  if (kPF && j0 < jend) load_col(Lnext, j0);
 #pragma unroll 1
   for (int j = j0; j < jend; ++j) {
-    LT L = Lnext;
-    if (j + 1 < jend) load_col(Lnext, j + 1);
+    LT L;
+    if constexpr (kPF)
+      L = Lnext;
+    else
+      load_col(L, j);
+    if (kPF && j + 1 < jend) load_col(Lnext, j + 1);
 #endif
 #ifndef ACOSS_NO_WINDOW8
 #ifndef ACOSS_NO_SAMPLE_HINT
@@ -1370,7 +1381,7 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
 // each pair picking its column line type (columns of at most short_n codes take LineS<8>);
 // KQ = 2: as 0, and columns past 2048 codes take Line2.
 template <int KQ>
-__global__ __launch_bounds__(256, KQ == 2 ? 3 : ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
+__global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
                                                    const uint32_t* __restrict__ RT, float* __restrict__ thr,
                                                    float* __restrict__ Tq, int64_t thr_stride,
                                                    uint32_t* __restrict__ maskT, int64_t mask_stride, int ld,
