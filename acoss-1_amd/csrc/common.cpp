@@ -62,16 +62,16 @@ void* workspace(int slot, size_t bytes) {
 
 // One extra stream and a few timing-free events per device, for overlapping independent
 // sub-batches inside one ABI call (the caller's stream stays the ordering point).
-hipStream_t side_stream() {
+hipStream_t side_stream(int idx) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  static std::map<int, hipStream_t> streams;
+  static std::map<std::pair<int, int>, hipStream_t> streams;
   std::lock_guard<std::mutex> lk(g_mu);
-  auto it = streams.find(dev);
+  auto it = streams.find({dev, idx});
   if (it != streams.end()) return it->second;
   hipStream_t st = nullptr;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  streams[dev] = st;
+  streams[{dev, idx}] = st;
   return st;
 }
 

@@ -16,7 +16,7 @@ void clear_error();
 // contents are not preserved on growth). Returns nullptr (and sets the error) on failure.
 void* workspace(int slot, size_t bytes);
 int release_all_workspaces();
-hipStream_t side_stream();      // per-device helper stream (non-blocking)
+hipStream_t side_stream(int idx = 0);  // per-device helper streams (non-blocking)
 hipEvent_t sync_event(int idx);  // per-device timing-free events for cross-stream ordering
 
 // Optional per-phase timing with HIP events recorded on the launch stream (bench.py reads it

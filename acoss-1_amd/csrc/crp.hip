@@ -1106,7 +1106,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   static const int nbuf = [] {
     const char* e = getenv("ACOSS_SPLIT_STREAMS");
     const int v = e ? atoi(e) : 2;
-    return v < 1 ? 1 : (v > 2 ? 2 : v);
+    return v < 1 ? 1 : (v > 3 ? 3 : v);
   }();
   char* ws = static_cast<char*>(workspace(1, slot * nb_alloc + (split ? nbuf * sub_pair * sub : 0) + 8192));
   if (!ws) return ACOSS_E_HIP;
@@ -1125,16 +1125,16 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   uint32_t* w_mask = reinterpret_cast<uint32_t*>(carve(4 * mask_stride * nb_alloc));
   float4* w_bnd = reinterpret_cast<float4*>(carve(16 * bnd_stride * nb_alloc));
   float* w_yrot = reinterpret_cast<float*>(carve(4 * yrot_stride * nb_alloc));
-  void* w_kpl[2] = {nullptr, nullptr};
-  uint32_t* w_rt[2] = {nullptr, nullptr};
+  void* w_kpl[3] = {nullptr, nullptr, nullptr};
+  uint32_t* w_rt[3] = {nullptr, nullptr, nullptr};
   for (int b = 0; split && b < nbuf; ++b) {
     w_kpl[b] = static_cast<void*>(carve(4 * (size_t)kstride * sub));
     w_rt[b] = reinterpret_cast<uint32_t*>(carve(4 * (size_t)mask_stride * sub));
   }
-  hipStream_t ss[2] = {s, s};
-  if (split && nbuf == 2) {
-    ss[1] = side_stream();
-    if (!ss[1]) {
+  hipStream_t ss[3] = {s, s, s};
+  for (int b = 1; split && b < nbuf; ++b) {
+    ss[b] = side_stream(b - 1);
+    if (!ss[b]) {
       set_error("could not create the side stream");
       return ACOSS_E_HIP;
     }
@@ -1153,16 +1153,17 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_OTI, s);
     if (split) {
-      const bool two = nbuf == 2 && nb > sub;
-      if (two) {  // the side stream starts after this batch's OTI / roll on the caller's stream
+      const int nsb = (int)((nb + sub - 1) / sub);     // sub-batches of this batch
+      const int nst = nbuf < nsb ? nbuf : nsb;         // streams they rotate over
+      if (nst > 1) {  // the side streams start after this batch's OTI / roll on the caller's stream
         hipEvent_t e0 = sync_event(0);
         ACOSS_HIP_CHECK(hipEventRecord(e0, s));
-        ACOSS_HIP_CHECK(hipStreamWaitEvent(ss[1], e0, 0));
+        for (int q = 1; q < nst; ++q) ACOSS_HIP_CHECK(hipStreamWaitEvent(ss[q], e0, 0));
       }
       int k = 0;
       for (int s0 = 0; s0 < nb; s0 += (int)sub, ++k) {
         const int ns = (nb - s0) < sub ? (nb - s0) : (int)sub;
-        const int b = two ? (k & 1) : 0;
+        const int b = k % nst;
         CrpBatch Bs{feats, X2, track_off, track_len, NX, ldn, pb + 2 * s0, w_oti + s0, w_dims + s0, m, tau,
                     w_yrot + (size_t)s0 * yrot_stride, yrot_stride};
         if ((rc = launch_crp_split(Bs, ns, L, params->kappa, w_kpl[b], ldk, kstride, w_rt[b],
@@ -1171,9 +1172,9 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
                                    w_mask + (size_t)s0 * mask_stride, mask_stride, ld, ss[b])))
           return rc;
       }
-      if (two) {  // the DP (caller's stream) needs every sub-batch of both streams
-        hipEvent_t e1 = sync_event(1);
-        ACOSS_HIP_CHECK(hipEventRecord(e1, ss[1]));
+      for (int q = 1; q < nst; ++q) {  // the DP (caller's stream) needs every sub-batch of every stream
+        hipEvent_t e1 = sync_event(q);
+        ACOSS_HIP_CHECK(hipEventRecord(e1, ss[q]));
         ACOSS_HIP_CHECK(hipStreamWaitEvent(s, e1, 0));
       }
     } else {
