@@ -557,12 +557,34 @@ struct Line {
 // so a wave-wide ballot of one mask bit is two consecutive 32-element words of the line (the
 // CRP's row and strip words) and every load is coalesced across the wave. KQ/2 packed words:
 // word h = element q = h (bits 0..15) and q = h + KQ/2 (bits 16..31); mask bit h <-> q = h and
-// bit h + 16 <-> q = h + KQ/2, the same flag gather as the long lines' split order. Plain
-// 16-bit search (no window codes: the counts are already KQ/2 words).
+// bit h + 16 <-> q = h + KQ/2, the same flag gather as the long lines' split order. KQ = 16
+// adds the long lines' 7-bit window codes (4 words: word h = elements q = h + 4k, k = 0..3, one
+// per byte; its flag gather puts q = h + 4k on bit h + 8k, which wmask moves to the 16-bit
+// layout's bits); KQ = 8 searches its 4 words directly.
 template <int KQ>
 struct LineS {
   static_assert(KQ == 8 || KQ == 16, "short lines: 8 or 16 elements per lane");
+  static constexpr bool kWin = KQ == 16;
   unsigned pv[KQ / 2];
+  unsigned w8[kWin ? KQ / 4 : 1];
+  unsigned base8;
+  bool win;
+  static constexpr uint32_t kWinLo = ((1u << (KQ / 4)) - 1u) * 0x10001u;
+  static __device__ __forceinline__ uint32_t wmask(uint32_t m) {
+    return (m & kWinLo) | ((m >> (8 - KQ / 4)) & (kWinLo << (KQ / 4)));
+  }
+  __device__ __forceinline__ void build_window(unsigned center) {
+    static_assert(kWin, "window codes: 16 codes per lane only");
+    base8 = center > 63u ? center - 63u : 0u;
+    win = true;
+    const unsigned B2 = base8 * 0x10001u;
+    unsigned c[KQ / 2];
+#pragma unroll
+    for (int h = 0; h < KQ / 2; ++h) c[h] = pk_min_u16(pk_subsat_u16(pv[h], B2), 0x007f007fu);
+#pragma unroll
+    for (int h = 0; h < KQ / 4; ++h) w8[h] = __builtin_amdgcn_perm(c[h + KQ / 4], c[h], 0x06020400u);
+  }
+  __device__ __forceinline__ bool in_win(unsigned x) const { return win && x >= base8 && x <= base8 + 126u; }
   static __device__ __forceinline__ int q_of_bit(int b) { return b < 16 ? b : b - 16 + KQ / 2; }
   static __device__ __forceinline__ int bit_of_q(int q) { return q < KQ / 2 ? q : q - KQ / 2 + 16; }
   __device__ __forceinline__ int ebase() const {
@@ -596,6 +618,10 @@ struct LineS {
   template <class AT>
   __device__ __forceinline__ void load(AT addr, int n) {
     const int lane = threadIdx.x & 63;
+    if constexpr (kWin) {
+      win = false;
+      base8 = 0u;
+    }
     unsigned v[KQ];
 #pragma unroll
     for (int q = 0; q < KQ; ++q) v[q] = *addr(min(lane + 64 * q, n - 1));
@@ -605,6 +631,15 @@ struct LineS {
     for (int h = 0; h < KQ / 2; ++h) pv[h] = v[h] | (v[h + KQ / 2] << 16);
   }
   __device__ __forceinline__ int count_le(unsigned x) const {
+    if constexpr (kWin) {
+      if (in_win(x)) {  // wave-uniform
+        const unsigned X4 = (x - base8 + 0x80u) * 0x01010101u;
+        unsigned c = 0;
+#pragma unroll
+        for (int h = 0; h < KQ / 4; ++h) c = __builtin_popcount((X4 - w8[h]) & 0x80808080u) + c;
+        return wave_sum((int)c);
+      }
+    }
     const unsigned X2 = (x + 0x8000u) * 0x10001u;
     unsigned c = 0;
 #pragma unroll
@@ -612,6 +647,15 @@ struct LineS {
     return wave_sum((int)c);
   }
   __device__ __forceinline__ uint32_t eq_mask(unsigned P) const {
+    if constexpr (kWin) {
+      if (in_win(P) && (P > base8 || base8 == 0u)) {  // code 0 is exact only when base8 == 0
+        const unsigned PP = (P - base8) * 0x01010101u;
+        uint32_t ne8 = 0;
+#pragma unroll
+        for (int h = 0; h < KQ / 4; ++h) ne8 = gather_flags8(ne8, (w8[h] ^ PP) + 0x7f7f7f7fu, h);
+        return wmask(~ne8);
+      }
+    }
     const unsigned PP = P * 0x10001u;
     uint32_t ne = 0;
 #pragma unroll
@@ -619,6 +663,15 @@ struct LineS {
     return ~ne & kMaskAll;
   }
   __device__ __forceinline__ uint32_t le_mask(unsigned x) const {
+    if constexpr (kWin) {
+      if (in_win(x)) {
+        const unsigned X4 = (x - base8 + 0x80u) * 0x01010101u;
+        uint32_t le8 = 0;
+#pragma unroll
+        for (int h = 0; h < KQ / 4; ++h) le8 = gather_flags8(le8, X4 - w8[h], h);
+        return wmask(le8);
+      }
+    }
     const unsigned X2 = (x + 0x8000u) * 0x10001u;
     uint32_t le = 0;
 #pragma unroll
@@ -1187,7 +1240,7 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
 #ifndef ACOSS_NO_SAMPLE_HINT
       if (hint.P == kNoHint) hint.P = sample_hint(L, V.Np, kappa);
 #endif
-      if constexpr (KQ == 0 || KQ == 2) {
+      if constexpr (KQ != 8) {
         if (hint.P != kNoHint) L.build_window(hint.P);
       }
 #endif
@@ -1203,7 +1256,7 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
       }
 #ifndef ACOSS_ABL_NOLEBITS
       word = le_bits(L, __builtin_bit_cast(unsigned, T), keyf, W, c_lo, c_hi);
-      if constexpr (KQ == 8) word = lane_words<KQ>((uint32_t)word);  // lane t: columns 32t .. 32t + 31
+      if constexpr (KQ == 8 || KQ == 16) word = lane_words<KQ>((uint32_t)word);  // lane t: columns 32t .. 32t + 31
 #endif
     }
     rowbits[r][lane] = (uint32_t)word;
@@ -1264,8 +1317,10 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
 #endif
   WaveLds* wl = reinterpret_cast<WaveLds*>(smem);
   uint32_t(*rowbits)[RB] = reinterpret_cast<uint32_t(*)[RB]>(smem + 4 * sizeof(WaveLds));
-  if (KQ == 8 || V.Np <= short_n)
+  if (KQ == 8 || (KQ != 16 && V.Np <= short_n))
     rows_body<4, 8, RB>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+  else if (KQ == 16)  // (mixed launches leave it out: a third select in one kernel costs more than it saves)
+    rows_body<4, 16, RB>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   else if (KQ == 2 && V.Np > 2048)
     rows_body<4, 2, RB>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   else
@@ -1289,7 +1344,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
 #define ACOSS_CPW_SHORT 4
 #endif
 template <int KQ>
-constexpr int kCPW = KQ == 8 ? ACOSS_CPW_SHORT : ACOSS_CPW;
+constexpr int kCPW = (KQ == 8 || KQ == 16) ? ACOSS_CPW_SHORT : ACOSS_CPW;
 #ifndef ACOSS_COLS_WPE
 #define ACOSS_COLS_WPE 4
 #endif
@@ -1342,7 +1397,7 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
 #ifndef ACOSS_NO_SAMPLE_HINT
     if (hint.P == kNoHint) hint.P = sample_hint(L, V.Mp, kappa);
 #endif
-    if constexpr (KQ == 0 || KQ == 2) {
+    if constexpr (KQ != 8) {
       if (hint.P != kNoHint) L.build_window(hint.P);
     }
 #endif
@@ -1367,7 +1422,7 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
     const uint64_t bits = 0;
 #else
     uint64_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
-    if constexpr (KQ == 8) bits = lane_words<KQ>((uint32_t)bits);  // lane s: rows 32s .. 32s + 31
+    if constexpr (KQ == 8 || KQ == 16) bits = lane_words<KQ>((uint32_t)bits);  // lane s: rows 32s .. 32s + 31
 #endif
     if (lane * KPL < V.Mp) maskT[w] = (uint32_t)bits & rt;
     if (KQ == 2 && 2048 + lane * KPL < V.Mp) maskT[w2] = (uint32_t)(bits >> 32) & rt2;
@@ -1394,8 +1449,10 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
   const int j0 = (lb - p * gridDim.x) * kColsPerBlock<KQ> + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCPW<KQ>;
   const int jend = min(j0 + kCPW<KQ>, V.Np);
   WaveLds& W = wl[threadIdx.x >> 6];
-  if (KQ == 8 || V.Mp <= short_n)
+  if (KQ == 8 || (KQ != 16 && V.Mp <= short_n))
     cols_body<8>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
+  else if (KQ == 16)
+    cols_body<16>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
   else if (KQ == 2 && V.Mp > 2048)
     cols_body<2>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
   else
@@ -1415,13 +1472,12 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
   const size_t plane = (size_t)nb * kstride;
   const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane};
   const int nstrips = (L + kSR - 1) / kSR;
-  // short lines (every line of the batch <= 512 codes) take the lane-strided selects. (16 codes
-  // per lane for lines <= 1024 measured the same as the long-line path, whose window codes
-  // already halve its count words, so only 8 is instantiated.)
-  // mixed batches: each pair picks per side (rows of <= 512 codes, columns of <= 512 codes)
+  // launches whose lines all fit 512 / 1024 codes take LineS<8> / LineS<16> throughout; in
+  // mixed launches each pair picks per side (lines of <= short_n codes LineS<8>, past 2048
+  // Line2, the rest Line<32>)
   static const bool no_short = getenv("ACOSS_NO_SHORT") != nullptr;
   const int short_n = no_short ? 0 : 512;
-  const int kq = L > 2048 ? 2 : ((!no_short && L <= 512) ? 8 : 0);  // 2: some line past 2048
+  const int kq = L > 2048 ? 2 : (no_short ? 0 : (L <= 512 ? 8 : (L <= 1024 ? 16 : 0)));  // 2: some line past 2048
   auto launch = [&](auto kqc) -> int {
     constexpr int KQ = decltype(kqc)::value;
     prof_begin(PH_SWEEP, s);
@@ -1437,6 +1493,7 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
     return ACOSS_OK;
   };
   if (kq == 8) return launch(std::integral_constant<int, 8>{});
+  if (kq == 16) return launch(std::integral_constant<int, 16>{});
   if (kq == 2) return launch(std::integral_constant<int, 2>{});
   return launch(std::integral_constant<int, 0>{});
 }
