@@ -182,3 +182,17 @@ def test_crp_align_long_lines():
     np.testing.assert_array_equal(got["oti"].cpu().numpy(), k)
     np.testing.assert_array_equal(got["qmax"].cpu().numpy(), q)
     np.testing.assert_array_equal(got["dmax"].cpu().numpy(), d)
+
+
+def test_crp_align_past_split_limit():
+    """A launch with a line of 4097 codes (a 4106-frame track) leaves the split path for the
+    generic fused kernels; results stay bit-exact."""
+    rng = np.random.Generator(np.random.PCG64(13))
+    tracks = [synthetic.render(rng, synthetic.base_sequence(rng, n)) for n in (300, 4106)]
+    feats, off, lens = synthetic.pack(tracks)
+    pairs = np.array([(0, 1), (1, 0)], np.int32)
+    q, d, k = oracle.crp_batch(feats, off, lens, pairs)
+    got = _lib.crp_align(feats, off, lens, int(lens.max()), pairs, _lib.crp_params(), qmax=True, dmax=True, oti=True)
+    np.testing.assert_array_equal(got["oti"].cpu().numpy(), k)
+    np.testing.assert_array_equal(got["qmax"].cpu().numpy(), q)
+    np.testing.assert_array_equal(got["dmax"].cpu().numpy(), d)
