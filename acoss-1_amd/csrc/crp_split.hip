@@ -833,18 +833,21 @@ struct Hint {
 // bisection (about nine counts) by a window search from the guess.
 template <class LT>
 __device__ __forceinline__ unsigned sample_hint(const LT& L, int n, float kappa) {
-  const int lane = threadIdx.x & 63;
-  unsigned v = L.sample();  // kNone on lanes whose sample is past the line
+  const unsigned v = L.sample();  // kNone on lanes whose sample is past the line
   const int ns = __popcll(__ballot(v != kNone));
   const int k = (int)((float)(n - 1) * kappa * (float)ns / (float)n);
+  // the k-th smallest sample: the least P with #(samples <= P) > k, by bisection over the
+  // samples' range with one ballot per step (no DPP chains)
+  unsigned lo = wave_min_u32(v), hi = wave_max_u32(v != kNone ? v : 0u);
 #pragma unroll 1
-  for (int r = 0; r < k; ++r) {
-    const unsigned m = wave_min_u32(v);
-    const int first = __builtin_ctzll(__ballot(v == m));
-    if (lane == first) v = 0xffffffffu;
+  while (lo < hi) {
+    const unsigned mid = (lo + hi) >> 1;
+    if (__popcll(__ballot(v <= mid)) > k)
+      hi = mid;
+    else
+      lo = mid + 1;
   }
-  const unsigned P = wave_min_u32(v);
-  return P > 0x7f80u ? 0x7f80u : P;
+  return lo > 0x7f80u ? 0x7f80u : lo;
 }
 
 // Scratch of one wave in LDS: element list and 64 bit-words.
