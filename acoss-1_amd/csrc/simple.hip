@@ -8,12 +8,25 @@
 //                         subsequences, score = median(MP). The reference builds QT with FFT
 //                         convolutions plus the STOMP update; here QT[i][j] = sum_t G[i+t][j+t]
 //                         with G the 12-term dot product of single frames (same value, different
-//                         rounding: parity is a tolerance, 1e-9 relative in the tests).
+//                         rounding: parity with the reference is a tolerance, 1e-9 relative in the
+//                         tests; with the oracle's canonical order it is bit-exact).
 //
-// One 256-thread block per pair. Thread t walks diagonals j - i = off of the (P x Q) profile
-// matrix: the last L G values live in a shift register, every completed window gives one
-// distance, folded into the row minimum with ds_min_u64 on order-preserving keys. The median
-// is an exact rank count over the P row minima in LDS.
+// Canonical rounding (oracle/crp_oracle.cpp or_simple_sim): frame dot products and frame norms
+// are the product of bin 0 and then an fma chain over bins 1..11, of the query and of the ROLLED
+// reference;
+// window sums are sequential adds t = 0..L-1; dist = (sb[j] + sa[i]) - 2 qt.
+//
+// Fast path (L = 10, the reference's SSLEN; k_simple_diag<K>): one 256-thread block per pair.
+// A wave owns 64·K consecutive diagonals o = j - i of the (P x Q) profile matrix, K adjacent
+// ones per lane, and walks down the rows: at step x every lane forms G(x, x + o) for its K
+// diagonals. The query frame x is wave-uniform (scalar loads); the K reference frames of a lane
+// are consecutive columns, so each step loads ONE new frame per lane and rotates the others (the
+// ring index is static after unrolling by lcm(10, K)). Each diagonal keeps its 10 open window
+// partials in registers (slot = start step mod 10), so every G is formed once and added into the
+// windows in the canonical order. All cells completed at step x lie in row x - 9: one DPP wave
+// minimum per step, one LDS atomic per row per wave. Frames live in a per-track frame-major
+// copy with the 12 bins stored twice, so the rolled reference frame is 12 contiguous doubles at
+// bin offset (12 - k) mod 12. The median is a bitonic sort of the row minima in LDS.
 #include "common.hpp"
 
 namespace acoss {
@@ -21,7 +34,9 @@ namespace acoss {
 namespace {
 
 constexpr int kMaxL = 16;
-constexpr int kMaxLen = 4096;  // LDS: 3 x 8 B x kMaxLen (window norms of a, b; row minima)
+constexpr int kMaxLen = 4096;  // frames per track (LDS: row minima + reference window norms)
+constexpr int kFastL = 10;     // simple_silva.py SSLEN
+constexpr int kExt = 24;       // doubles per frame in the frame-major copy (bins 0..11 twice)
 
 __device__ __forceinline__ unsigned long long dkey(double v) {
   const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
@@ -32,10 +47,27 @@ __device__ __forceinline__ double dkey_inv(unsigned long long k) {
   return __builtin_bit_cast(double, u);
 }
 
-// per-track chroma profile (sum over time, sequential) and per-frame squared norms
+// Simple.oti: v[k] = dot(p_a, roll(p_b, k)); argsort(v)[-1] -> last index of the maximum
+__device__ int simple_oti_index(const double* pa, const double* pb) {
+  int best = 0;
+  double bv = 0.0;
+  for (int k = 0; k < 12; ++k) {
+    double acc = 0.0;
+    for (int c = 0; c < 12; ++c) acc = acc + pa[c] * pb[(c - k + 12) % 12];
+    if (k == 0 || acc >= bv) {
+      bv = acc;
+      best = k;
+    }
+  }
+  return best;
+}
+
+// per-track chroma profile (sum over time, sequential), per-frame squared norms (fma chain),
+// the frame-major doubled copy ext[t][x][0..23], and the L-window norms of the unrolled track
 __global__ void k_simple_track(const double* __restrict__ feats, const int64_t* __restrict__ off,
-                               const int32_t* __restrict__ len, int n_tracks, double* __restrict__ prof,
-                               double* __restrict__ fnorm, int64_t ldf) {
+                               const int32_t* __restrict__ len, int n_tracks, int L, double* __restrict__ prof,
+                               double* __restrict__ fnorm, double* __restrict__ wnorm, double* __restrict__ ext,
+                               int64_t ldf) {
   const int tr = blockIdx.x;
   if (tr >= n_tracks) return;
   const double* S = feats + off[tr];
@@ -46,19 +78,29 @@ __global__ void k_simple_track(const double* __restrict__ feats, const int64_t* 
     for (int x = 0; x < n; ++x) acc = acc + S[(size_t)t * n + x];
     prof[tr * 12 + t] = acc;
   }
+  double* E = ext + (size_t)tr * ldf * kExt;
   for (int x = t; x < n; x += blockDim.x) {
     double acc = 0.0;
     for (int d = 0; d < 12; ++d) {
       const double v = S[(size_t)d * n + x];
-      acc = acc + v * v;
+      acc = d == 0 ? v * v : fma(v, v, acc);
+      E[(size_t)x * kExt + d] = v;
+      E[(size_t)x * kExt + 12 + d] = v;
     }
     fnorm[(size_t)tr * ldf + x] = acc;
   }
+  __syncthreads();
+  for (int i = t; i + L <= n; i += blockDim.x) {
+    double acc = 0.0;
+    for (int u = 0; u < L; ++u) acc = acc + fnorm[(size_t)tr * ldf + i + u];
+    wnorm[(size_t)tr * ldf + i] = acc;
+  }
 }
 
+// Generic sslen (1..16): one thread per diagonal, L-deep shift register of G.
 __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ feats, const int64_t* __restrict__ off,
                                                      const int32_t* __restrict__ len, const int32_t* __restrict__ pairs,
-                                                     const double* __restrict__ prof, const double* __restrict__ fnorm,
+                                                     const double* __restrict__ prof, const double* __restrict__ wnorm,
                                                      int64_t ldf, int L, int apply_oti, double* __restrict__ score,
                                                      int32_t* __restrict__ oti_out) {
   __shared__ double sa[kMaxLen];
@@ -74,19 +116,7 @@ __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ 
   const double* B = feats + off[tb];
   const int P = na - L + 1, Q = nb - L + 1;
   if (t == 0) {
-    // Simple.oti: v[k] = dot(p_a, roll(p_b, k)); argsort(v)[-1] -> last index of the maximum
-    const double* pa = prof + ta * 12;
-    const double* pb = prof + tb * 12;
-    int best = 0;
-    double bv = 0.0;
-    for (int k = 0; k < 12; ++k) {
-      double acc = 0.0;
-      for (int c = 0; c < 12; ++c) acc = acc + pa[c] * pb[(c - k + 12) % 12];
-      if (k == 0 || acc >= bv) {
-        bv = acc;
-        best = k;
-      }
-    }
+    const int best = simple_oti_index(prof + ta * 12, prof + tb * 12);
     s_k = apply_oti ? best : 0;
     if (oti_out) oti_out[p] = best;
   }
@@ -94,12 +124,8 @@ __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ 
     if (t == 0) score[p] = __builtin_nan("");
     return;
   }
-  // query window norms: sequential sums of L frame norms
-  const double* fa = fnorm + (size_t)ta * ldf;
   for (int i = t; i < P; i += 256) {
-    double acc = 0.0;
-    for (int u = 0; u < L; ++u) acc = acc + fa[i + u];
-    sa[i] = acc;
+    sa[i] = wnorm[(size_t)ta * ldf + i];
     mpk[i] = ~0ull;
   }
   __syncthreads();
@@ -111,11 +137,11 @@ __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ 
   for (int j = t; j < Q; j += 256) {
     double acc = 0.0;
     for (int u = 0; u < L; ++u) {
-      double f = 0.0;
+      double f = B[rowB[0] + j + u] * B[rowB[0] + j + u];
 #pragma unroll
-      for (int c = 0; c < 12; ++c) {
+      for (int c = 1; c < 12; ++c) {
         const double v = B[rowB[c] + j + u];
-        f = f + v * v;
+        f = fma(v, v, f);
       }
       acc = acc + f;
     }
@@ -131,9 +157,9 @@ __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ 
     for (int u = 0; u < kMaxL; ++u) buf[u] = 0.0;
     for (int x = r0; x <= r1 + L - 1; ++x) {
       const int y = x + o;
-      double g = 0.0;
+      double g = A[x] * B[rowB[0] + y];
 #pragma unroll
-      for (int c = 0; c < 12; ++c) g = g + A[(size_t)c * na + x] * B[rowB[c] + y];
+      for (int c = 1; c < 12; ++c) g = fma(A[(size_t)c * na + x], B[rowB[c] + y], g);
 #pragma unroll
       for (int u = 0; u < kMaxL - 1; ++u) buf[u] = buf[u + 1];
       buf[kMaxL - 1] = g;
@@ -159,7 +185,6 @@ __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ 
       less += v < me;
       eq += v == me;
     }
-    // the first holder (lowest index) of a tied value writes
     int first = 1;
     for (int f = 0; f < e; ++f) first &= mpk[f] != me;
     if (first) {
@@ -169,6 +194,221 @@ __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ 
   }
   __syncthreads();
   if (t == 0) score[p] = (P % 2) ? s_med[1] : 0.5 * (s_med[0] + s_med[1]);
+}
+
+// ---- fast path: L = 10, K adjacent diagonals per lane ----
+
+typedef __attribute__((address_space(4))) double CDouble;  // scalar (s_load) path for uniform loads
+
+// v_min_f64 without fmin's NaN canonicalisation (IEEE minNum: a NaN operand yields the other)
+__device__ __forceinline__ double vmin_f64(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Wave minimum of a double (DPP row_shr 1/2/4/8, row_bcast 15/31; total in lane 63).
+__device__ __forceinline__ double wave_min_f64(double v) {
+  const unsigned IHI = 0x7ff00000u;  // +inf: lo 0, hi 0x7ff00000
+#define ACOSS_MIN_STAGE(CTRL, RM)                                                                     \
+  {                                                                                                 \
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);                         \
+    const unsigned lo = dpp_u32<CTRL, RM>(0u, (unsigned)u);                                         \
+    const unsigned hi = dpp_u32<CTRL, RM>(IHI, (unsigned)(u >> 32));                                \
+    v = vmin_f64(v, __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo));               \
+  }
+  ACOSS_MIN_STAGE(0x111, 0xf)
+  ACOSS_MIN_STAGE(0x112, 0xf)
+  ACOSS_MIN_STAGE(0x114, 0xf)
+  ACOSS_MIN_STAGE(0x118, 0xf)
+  ACOSS_MIN_STAGE(0x142, 0xa)
+  ACOSS_MIN_STAGE(0x143, 0xc)
+#undef ACOSS_MIN_STAGE
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, 63);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), 63);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+constexpr int gcd_c(int a, int b) { return b == 0 ? a : gcd_c(b, a % b); }
+
+// Row minima of one unrolled chunk of U steps through LDS (RED = 1): every step stores the lane
+// minima m (one row per step) to the wave's rbuf[step][lane]; after the chunk, S = 64 / U lanes
+// per row each fold a 16-B aligned segment of that row and ds_min the key (at most S-way).
+constexpr int kRbufStride = 72;  // doubles per rbuf row: 64 lanes + pad (+inf) for the segments
+
+template <int K, int RED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_simple_diag(const double* __restrict__ ext, const int32_t* __restrict__ len,
+                                                     const int32_t* __restrict__ pairs, const double* __restrict__ prof,
+                                                     const double* __restrict__ wnorm, int64_t ldf, int n2max,
+                                                     int sboff, int rboff, int apply_oti, double* __restrict__ score,
+                                                     int32_t* __restrict__ oti_out) {
+  constexpr int L = kFastL;
+  constexpr int U = L * K / gcd_c(L, K);  // unroll: window slots (mod L) and frame ring (mod K) static
+  extern __shared__ unsigned long long smem[];
+  unsigned long long* mpk = smem;                               // n2max row-minimum keys (sort buffer)
+  double* sb = reinterpret_cast<double*>(smem + sboff);         // reference window norms (rolled)
+  __shared__ int s_k;
+  const int p = blockIdx.x;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);  // wave: SGPR
+  const int ta = pairs[2 * p], tb = pairs[2 * p + 1];
+  const int na = len[ta], nb = len[tb];
+  const int P = na - L + 1, Q = nb - L + 1;
+  if (t == 0) {
+    const int best = simple_oti_index(prof + ta * 12, prof + tb * 12);
+    s_k = apply_oti ? best : 0;
+    if (oti_out) oti_out[p] = best;
+  }
+  if (P <= 0 || Q <= 0) {
+    if (t == 0) score[p] = __builtin_nan("");
+    return;
+  }
+  __syncthreads();
+  const int shift = __builtin_amdgcn_readfirstlane((12 - s_k) % 12);  // Brot[c] = ext[y][shift + c]
+  const double* Ea = ext + (size_t)ta * ldf * kExt;
+  const double* Eb = ext + (size_t)tb * ldf * kExt + shift;
+  const double* Wa = wnorm + (size_t)ta * ldf;
+  // rolled reference frame norms (fma chain over Brot's bins 0..11) into the key buffer, then
+  // the window sums into sb
+  double* fn = reinterpret_cast<double*>(mpk);
+  for (int y = t; y < nb; y += 256) {
+    double acc = Eb[(size_t)y * kExt] * Eb[(size_t)y * kExt];
+#pragma unroll
+    for (int c = 1; c < 12; ++c) {
+      const double v = Eb[(size_t)y * kExt + c];
+      acc = fma(v, v, acc);
+    }
+    fn[y] = acc;
+  }
+  __syncthreads();
+  for (int j = t; j < Q; j += 256) {
+    double acc = fn[j];
+#pragma unroll
+    for (int u = 1; u < L; ++u) acc = acc + fn[j + u];
+    sb[j] = acc;
+  }
+  __syncthreads();
+  const int n2 = n2max;
+  for (int i = t; i < n2; i += 256) mpk[i] = ~0ull;
+  constexpr int RS = 64 / U;                  // lanes per row in the chunk reduction
+  constexpr int RSEG = ((64 + RS - 1) / RS + 1) / 2 * 2;  // segment length (even: b128 reads)
+  static_assert(RS * RSEG <= kRbufStride, "rbuf pad");
+  double* rbuf = reinterpret_cast<double*>(smem + rboff) + wave * (U * kRbufStride);
+  if (RED) {
+    for (int i = lane; i < U * kRbufStride; i += 64) rbuf[i] = __builtin_inf();
+  }
+  __syncthreads();
+
+  constexpr int DW = 64 * K;  // diagonals per wave group
+  const int ND = P + Q - 1;
+  const int NG = (ND + DW - 1) / DW;
+  const double kInf = __builtin_inf();
+  for (int g = wave; g < NG; g += 4) {
+    const int ob = -(P - 1) + g * DW;  // diagonal of lane 0, k = 0
+    const int x_lo = max(0, -(ob + DW - 1));
+    const int x_hi = min(P - 1, Q - 1 - ob) + L - 1;
+    const int xs = x_lo - x_lo % U;
+    const int yl = ob + K * lane;  // column of diagonal k at step x: x + yl + k
+    double F[K][12];
+    double SB[K];
+    double part[K][L];
+    auto load_frame = [&](int slot, int y) {
+      const int yc = min(max(y, 0), nb - 1);
+      const double* src = Eb + (size_t)yc * kExt;
+#pragma unroll
+      for (int c = 0; c < 12; ++c) F[slot][c] = src[c];
+      const int cc = y - (L - 1);  // the cell column this frame closes
+      SB[slot] = (cc >= 0 && cc < Q) ? sb[cc] : kInf;
+    };
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) load_frame(k, xs + yl + k);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int s = 0; s < L; ++s) part[k][s] = 0.0;
+    for (int x0 = xs; x0 <= x_hi; x0 += U) {
+#pragma unroll
+      for (int ph = 0; ph < U; ++ph) {
+        const int x = x0 + ph;
+        load_frame((ph + K - 1) % K, x + yl + K - 1);
+        // wave-uniform query frame and window norm: scalar loads (constant address space)
+        const CDouble* Arow = (const CDouble*)(Ea + (size_t)min(x, na - 1) * kExt);
+        double a[12];
+#pragma unroll
+        for (int c = 0; c < 12; ++c) a[c] = Arow[c];
+        const int r = x - (L - 1);
+        const bool emit = r >= 0 && r < P;
+        const double sar = *(const CDouble*)(Wa + min(max(r, 0), P - 1));
+        double m = kInf;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int slot = (ph + k) % K;
+          double gv = a[0] * F[slot][0];
+#pragma unroll
+          for (int c = 1; c < 12; ++c) gv = fma(a[c], F[slot][c], gv);
+          const int s0 = ph % L;
+          part[k][s0] = gv;
+#pragma unroll
+          for (int j = 1; j < L; ++j) {
+            const int s = (ph - j + L) % L;
+            part[k][s] = part[k][s] + gv;
+          }
+          const double qt = part[k][(ph + 1) % L];
+          m = vmin_f64(m, fma(-2.0, qt, SB[slot] + sar));
+        }
+        if (RED) {
+          rbuf[ph * kRbufStride + lane] = m;
+        } else if (emit) {
+          const double wm = wave_min_f64(m);
+          if (lane == 0 && wm < kInf) atomicMin(&mpk[r], dkey(wm));
+        }
+      }
+      if (RED) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int ph = lane / RS, seg = lane % RS;
+        const int r = x0 + ph - (L - 1);
+        if (ph < U && r >= 0 && r < P) {
+          const double* src = rbuf + ph * kRbufStride + seg * RSEG;
+          double v = src[0];
+#pragma unroll 1
+          for (int i = 1; i < RSEG; i += 1) v = vmin_f64(v, src[i]);
+          if (v < kInf) atomicMin(&mpk[r], dkey(v));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+  }
+  __syncthreads();
+  // bitonic sort of the n2 keys (pads are ~0 and sort last)
+  for (int kk = 2; kk <= n2; kk <<= 1) {
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < n2; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long a = mpk[i], b = mpk[ixj];
+          const bool up = (i & kk) == 0;
+          if ((a > b) == up) {
+            mpk[i] = b;
+            mpk[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (t == 0)
+    score[p] = (P % 2) ? dkey_inv(mpk[P / 2]) : 0.5 * (dkey_inv(mpk[P / 2 - 1]) + dkey_inv(mpk[P / 2]));
+}
+
+int pow2_at_least(int v) {
+  int p = 2;
+  while (p < v) p <<= 1;
+  return p;
 }
 
 }  // namespace
@@ -196,18 +436,41 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   prof_begin(PH_SIMPLE, s);
   const int64_t ldf = (int64_t)align_up((size_t)max(max_len, 1), 64);
-  const size_t bytes = align_up((size_t)n_tracks * 12 * 8, 256) + (size_t)n_tracks * ldf * 8;
+  const size_t prof_bytes = align_up((size_t)n_tracks * 12 * 8, 256);
+  const size_t vec_bytes = (size_t)n_tracks * ldf * 8;
+  const size_t bytes = prof_bytes + 2 * vec_bytes + vec_bytes * kExt;
   char* ws = static_cast<char*>(workspace(8, bytes));
   if (!ws) return ACOSS_E_HIP;
   double* prof = reinterpret_cast<double*>(ws);
-  double* fnorm = reinterpret_cast<double*>(ws + align_up((size_t)n_tracks * 12 * 8, 256));
-  hipLaunchKernelGGL(k_simple_track, dim3(n_tracks), dim3(256), 0, s, feats, track_off, track_len, n_tracks, prof,
-                     fnorm, ldf);
+  double* fnorm = reinterpret_cast<double*>(ws + prof_bytes);
+  double* wnorm = reinterpret_cast<double*>(ws + prof_bytes + vec_bytes);
+  double* ext = reinterpret_cast<double*>(ws + prof_bytes + 2 * vec_bytes);
+  hipLaunchKernelGGL(k_simple_track, dim3(n_tracks), dim3(256), 0, s, feats, track_off, track_len, n_tracks, sslen,
+                     prof, fnorm, wnorm, ext, ldf);
   ACOSS_LAUNCH_CHECK();
+  const char* kenv = getenv("ACOSS_SIMPLE_K");
+  const int kdiag = kenv ? atoi(kenv) : (max_len > 512 ? 4 : 2);
+  const int n2max = pow2_at_least(max(max_len - kFastL + 1, 2));
+  const int sboff = max(n2max, (int)max_len);  // the key buffer also holds nb frame norms first
+  const int rboff = sboff + (int)align_up((size_t)max_len, 2);
+  const char* renv = getenv("ACOSS_SIMPLE_RED");
+  const int red = renv ? atoi(renv) : 1;
+  const int U = kdiag == 4 ? 20 : 10;
+  const size_t lds = ((size_t)rboff + (red ? (size_t)4 * U * kRbufStride : 0)) * 8;
   for (int64_t p0 = 0; p0 < n_pairs; p0 += 1 << 20) {
     const int64_t np = std::min<int64_t>(n_pairs - p0, 1 << 20);
-    hipLaunchKernelGGL(k_simple_pair, dim3((unsigned)np), dim3(256), 0, s, feats, track_off, track_len, pairs + 2 * p0,
-                       prof, fnorm, ldf, sslen, apply_oti, score_out + p0, oti_out ? oti_out + p0 : nullptr);
+    const int32_t* pp = pairs + 2 * p0;
+    double* so = score_out + p0;
+    int32_t* oo = oti_out ? oti_out + p0 : nullptr;
+    if (sslen == kFastL && (kdiag == 4 || kdiag == 2)) {
+      auto kern = kdiag == 4 ? (red ? k_simple_diag<4, 1> : k_simple_diag<4, 0>)
+                             : (red ? k_simple_diag<2, 1> : k_simple_diag<2, 0>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)np), dim3(256), lds, s, ext, track_len, pp, prof, wnorm, ldf, n2max,
+                         sboff, rboff, apply_oti, so, oo);
+    } else {
+      hipLaunchKernelGGL(k_simple_pair, dim3((unsigned)np), dim3(256), 0, s, feats, track_off, track_len, pp, prof,
+                         wnorm, ldf, sslen, apply_oti, so, oo);
+    }
     ACOSS_LAUNCH_CHECK();
   }
   prof_end(PH_SIMPLE, s);

@@ -279,7 +279,9 @@ double or_sw_constrained(const uint8_t* B, int M, int N) {
 }
 
 // acoss Simple.simple_sim (simple_silva.py:68-118): median over i of
-// min_j ||A[:, i:i+L] - B[:, j:j+L]||^2 computed as sa + sb - 2 QT (float64).
+// min_j ||A[:, i:i+L] - B[:, j:j+L]||^2 computed as sa + sb - 2 QT (float64). Canonical order
+// (shared with simple.hip): frame dots and frame norms are a product of bin 0 then an fma chain over bins 1..11,
+// window sums are sequential adds.
 // A: 12 x na, B: 12 x nb, both row-major (dim-major) as in the reference.
 double or_simple_sim(const double* A, int na, const double* B, int nb, int L) {
   const int P = na - L + 1, Q = nb - L + 1;
@@ -287,19 +289,19 @@ double or_simple_sim(const double* A, int na, const double* B, int nb, int L) {
   std::vector<double> ga((size_t)na * nb);
   for (int x = 0; x < na; ++x)
     for (int y = 0; y < nb; ++y) {
-      double acc = 0.0;
-      for (int d = 0; d < 12; ++d) acc += A[(size_t)d * na + x] * B[(size_t)d * nb + y];
+      double acc = A[x] * B[y];
+      for (int d = 1; d < 12; ++d) acc = std::fma(A[(size_t)d * na + x], B[(size_t)d * nb + y], acc);
       ga[(size_t)x * nb + y] = acc;
     }
   std::vector<double> na2(na), nb2(nb), sa(P), sb(Q), mp(P);
   for (int x = 0; x < na; ++x) {
-    double acc = 0.0;
-    for (int d = 0; d < 12; ++d) acc += A[(size_t)d * na + x] * A[(size_t)d * na + x];
+    double acc = A[x] * A[x];
+    for (int d = 1; d < 12; ++d) acc = std::fma(A[(size_t)d * na + x], A[(size_t)d * na + x], acc);
     na2[x] = acc;
   }
   for (int y = 0; y < nb; ++y) {
-    double acc = 0.0;
-    for (int d = 0; d < 12; ++d) acc += B[(size_t)d * nb + y] * B[(size_t)d * nb + y];
+    double acc = B[y] * B[y];
+    for (int d = 1; d < 12; ++d) acc = std::fma(B[(size_t)d * nb + y], B[(size_t)d * nb + y], acc);
     nb2[y] = acc;
   }
   for (int i = 0; i < P; ++i) {

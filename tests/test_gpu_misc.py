@@ -188,3 +188,27 @@ def test_simple_batch_vs_oracle(lib):
         assert oti[p] == k
         ref = oracle.simple_sim(feats[i], np.roll(feats[j], k, axis=0), 10)
         assert score[p] == ref or (np.isnan(ref) and np.isnan(score[p]))
+
+
+@pytest.mark.parametrize("sslen,kdiag", [(10, None), (10, "2"), (10, "4"), (7, None)])
+def test_simple_long_vs_oracle(lib, monkeypatch, sslen, kdiag):
+    """Fast diagonal kernel (L = 10, K = 2 / 4 diagonals per lane) and the generic sslen path on
+    tracks up to 1300 frames with unequal lengths (ragged diagonal groups), bit-exact."""
+    if kdiag is not None:
+        monkeypatch.setenv("ACOSS_SIMPLE_K", kdiag)
+    rng = np.random.default_rng(5 + sslen)
+    feats = []
+    for n in [9, 10, 700, 1300, 513, 96]:
+        F = np.abs(rng.standard_normal((12, n)))
+        F /= np.linalg.norm(F, axis=0, keepdims=True)
+        feats.append(F)
+    feats.append(feats[2].copy())  # identical tracks: zero distances
+    pairs = np.array([(i, j) for i in range(len(feats)) for j in range(len(feats)) if (i + j) % 2 == 0 or i == 6],
+                     dtype=np.int32)
+    score, oti = lib.simple_mp(feats, pairs, sslen=sslen)
+    score, oti = _np(score), _np(oti)
+    for p, (i, j) in enumerate(pairs):
+        k = oracle.simple_oti(feats[i], feats[j])
+        assert oti[p] == k
+        ref = oracle.simple_sim(feats[i], np.roll(feats[j], k, axis=0), sslen)
+        assert score[p] == ref or (np.isnan(ref) and np.isnan(score[p])), (i, j, score[p], ref)
