@@ -241,38 +241,41 @@ template <int K, int RED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_simple_diag(const double* __restrict__ ext, const int32_t* __restrict__ len,
                                                      const int32_t* __restrict__ pairs, const double* __restrict__ prof,
                                                      const double* __restrict__ wnorm, int64_t ldf, int n2max,
-                                                     int sboff, int rboff, int apply_oti, double* __restrict__ score,
+                                                     int sboff, int slotsz, int rboff, int ppb, int64_t n_pairs,
+                                                     int apply_oti, double* __restrict__ score,
                                                      int32_t* __restrict__ oti_out) {
   constexpr int L = kFastL;
   constexpr int U = L * K / gcd_c(L, K);  // unroll: window slots (mod L) and frame ring (mod K) static
   extern __shared__ unsigned long long smem[];
-  unsigned long long* mpk = smem;                               // n2max row-minimum keys (sort buffer)
-  double* sb = reinterpret_cast<double*>(smem + sboff);         // reference window norms (rolled)
-  __shared__ int s_k;
-  const int p = blockIdx.x;
+  __shared__ int s_k[4];
+  // ppb pairs per block (short tracks: a pair has fewer than 4 diagonal groups); WPP waves each
   const int t = threadIdx.x;
   const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);  // wave: SGPR
-  const int ta = pairs[2 * p], tb = pairs[2 * p + 1];
+  const int WPP = 4 / ppb, slot = wave / WPP, lw = wave % WPP;
+  const int nthr = 64 * WPP, tl = t - slot * nthr;
+  unsigned long long* mpk = smem + (size_t)slot * slotsz;                // n2max row-minimum keys
+  double* sb = reinterpret_cast<double*>(mpk + sboff);                  // reference window norms (rolled)
+  const int64_t p = (int64_t)blockIdx.x * ppb + slot;
+  const bool active = p < n_pairs;
+  const int ta = active ? pairs[2 * p] : 0, tb = active ? pairs[2 * p + 1] : 0;
   const int na = len[ta], nb = len[tb];
   const int P = na - L + 1, Q = nb - L + 1;
-  if (t == 0) {
+  const bool live = active && P > 0 && Q > 0;
+  if (active && tl == 0) {
     const int best = simple_oti_index(prof + ta * 12, prof + tb * 12);
-    s_k = apply_oti ? best : 0;
+    s_k[slot] = apply_oti ? best : 0;
     if (oti_out) oti_out[p] = best;
-  }
-  if (P <= 0 || Q <= 0) {
-    if (t == 0) score[p] = __builtin_nan("");
-    return;
+    if (!live) score[p] = __builtin_nan("");
   }
   __syncthreads();
-  const int shift = __builtin_amdgcn_readfirstlane((12 - s_k) % 12);  // Brot[c] = ext[y][shift + c]
+  const int shift = live ? __builtin_amdgcn_readfirstlane((12 - s_k[slot]) % 12) : 0;  // Brot[c] = ext[y][shift + c]
   const double* Ea = ext + (size_t)ta * ldf * kExt;
   const double* Eb = ext + (size_t)tb * ldf * kExt + shift;
   const double* Wa = wnorm + (size_t)ta * ldf;
   // rolled reference frame norms (fma chain over Brot's bins 0..11) into the key buffer, then
   // the window sums into sb
   double* fn = reinterpret_cast<double*>(mpk);
-  for (int y = t; y < nb; y += 256) {
+  for (int y = tl; live && y < nb; y += nthr) {
     double acc = Eb[(size_t)y * kExt] * Eb[(size_t)y * kExt];
 #pragma unroll
     for (int c = 1; c < 12; ++c) {
@@ -282,7 +285,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     fn[y] = acc;
   }
   __syncthreads();
-  for (int j = t; j < Q; j += 256) {
+  for (int j = tl; live && j < Q; j += nthr) {
     double acc = fn[j];
 #pragma unroll
     for (int u = 1; u < L; ++u) acc = acc + fn[j + u];
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
   __syncthreads();
   const int n2 = n2max;
-  for (int i = t; i < n2; i += 256) mpk[i] = ~0ull;
+  for (int i = tl; i < n2; i += nthr) mpk[i] = ~0ull;
   constexpr int RS = 64 / U;                  // lanes per row in the chunk reduction
   constexpr int RSEG = ((64 + RS - 1) / RS + 1) / 2 * 2;  // segment length (even: b128 reads)
   static_assert(RS * RSEG <= kRbufStride, "rbuf pad");
@@ -302,9 +305,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
   constexpr int DW = 64 * K;  // diagonals per wave group
   const int ND = P + Q - 1;
-  const int NG = (ND + DW - 1) / DW;
+  const int NG = live ? (ND + DW - 1) / DW : 0;
   const double kInf = __builtin_inf();
-  for (int g = wave; g < NG; g += 4) {
+  for (int g = lw; g < NG; g += WPP) {
     const int ob = -(P - 1) + g * DW;  // diagonal of lane 0, k = 0
     const int x_lo = max(0, -(ob + DW - 1));
     const int x_hi = min(P - 1, Q - 1 - ob) + L - 1;
@@ -387,7 +390,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   // bitonic sort of the n2 keys (pads are ~0 and sort last)
   for (int kk = 2; kk <= n2; kk <<= 1) {
     for (int j = kk >> 1; j > 0; j >>= 1) {
-      for (int i = t; i < n2; i += 256) {
+      for (int i = tl; i < n2; i += nthr) {
         const int ixj = i ^ j;
         if (ixj > i) {
           const unsigned long long a = mpk[i], b = mpk[ixj];
@@ -401,7 +404,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       __syncthreads();
     }
   }
-  if (t == 0)
+  if (live && tl == 0)
     score[p] = (P % 2) ? dkey_inv(mpk[P / 2]) : 0.5 * (dkey_inv(mpk[P / 2 - 1]) + dkey_inv(mpk[P / 2]));
 }
 
@@ -449,24 +452,33 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
                      prof, fnorm, wnorm, ext, ldf);
   ACOSS_LAUNCH_CHECK();
   const char* kenv = getenv("ACOSS_SIMPLE_K");
-  const int kdiag = kenv ? atoi(kenv) : (max_len > 512 ? 4 : 2);
+  const int kdiag = kenv ? atoi(kenv) : 4;
   const int n2max = pow2_at_least(max(max_len - kFastL + 1, 2));
   const int sboff = max(n2max, (int)max_len);  // the key buffer also holds nb frame norms first
-  const int rboff = sboff + (int)align_up((size_t)max_len, 2);
-  const char* renv = getenv("ACOSS_SIMPLE_RED");
-  const int red = renv ? atoi(renv) : 1;
+  const int slotsz = sboff + (int)align_up((size_t)max_len, 2);
   const int U = kdiag == 4 ? 20 : 10;
+  // pairs per block: a block's 4 waves stay busy when a pair has fewer than 4 diagonal groups
+  const int ngmax = (2 * max(max_len - kFastL + 1, 1) - 1 + 64 * kdiag - 1) / (64 * kdiag);
+  const int ppb = ngmax <= 1 ? 4 : (ngmax <= 2 ? 2 : 1);
+  // row minima through LDS chunks for packed short pairs, per-step DPP minima for long ones
+  // (measured: 200 frames 5.85M vs 5.58M pairs/s, 2000 frames 48.0k vs 51.0k)
+  const char* renv = getenv("ACOSS_SIMPLE_RED");
+  const int red = renv ? atoi(renv) : (ppb > 1 ? 1 : 0);
+  const int rboff = ppb * slotsz;
   const size_t lds = ((size_t)rboff + (red ? (size_t)4 * U * kRbufStride : 0)) * 8;
-  for (int64_t p0 = 0; p0 < n_pairs; p0 += 1 << 20) {
-    const int64_t np = std::min<int64_t>(n_pairs - p0, 1 << 20);
+  for (int64_t p0 = 0; p0 < n_pairs; p0 += (int64_t)ppb << 20) {
+    const int64_t np = std::min<int64_t>(n_pairs - p0, (int64_t)ppb << 20);
     const int32_t* pp = pairs + 2 * p0;
     double* so = score_out + p0;
     int32_t* oo = oti_out ? oti_out + p0 : nullptr;
     if (sslen == kFastL && (kdiag == 4 || kdiag == 2)) {
       auto kern = kdiag == 4 ? (red ? k_simple_diag<4, 1> : k_simple_diag<4, 0>)
                              : (red ? k_simple_diag<2, 1> : k_simple_diag<2, 0>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)np), dim3(256), lds, s, ext, track_len, pp, prof, wnorm, ldf, n2max,
-                         sboff, rboff, apply_oti, so, oo);
+      if (lds > 64 * 1024)
+        ACOSS_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(kern, dim3((unsigned)((np + ppb - 1) / ppb)), dim3(256), lds, s, ext, track_len, pp, prof,
+                         wnorm, ldf, n2max, sboff, slotsz, rboff, ppb, np, apply_oti, so, oo);
     } else {
       hipLaunchKernelGGL(k_simple_pair, dim3((unsigned)np), dim3(256), 0, s, feats, track_off, track_len, pp, prof,
                          wnorm, ldf, sslen, apply_oti, so, oo);

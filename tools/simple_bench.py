@@ -20,6 +20,9 @@ from acoss import _lib  # noqa: E402
 import oracle  # noqa: E402
 
 
+VARIANTS = [("1", "1"), ("2", "0"), ("2", "1"), ("4", "0"), ("4", "1")]
+
+
 def run(n, n_tracks, reps, check):
     rng = np.random.default_rng(7)
     feats = []
@@ -36,7 +39,7 @@ def run(n, n_tracks, reps, check):
         k = oracle.simple_oti(feats[i], feats[j])
         ref.append(oracle.simple_sim(feats[i], np.roll(feats[j], k, axis=0)))
     out = {}
-    for kd, red in [("1", "1"), ("2", "0"), ("2", "1"), ("4", "0"), ("4", "1")]:
+    for kd, red in VARIANTS:
         os.environ["ACOSS_SIMPLE_RED"] = red
         os.environ["ACOSS_SIMPLE_K"] = kd
         score, _ = _lib.simple_mp_packed(flat, off, lens, pt)
@@ -56,8 +59,14 @@ def run(n, n_tracks, reps, check):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "simple_ab.json"))
+    ap.add_argument("--frames", type=int, nargs="*", default=[200, 2000])
+    ap.add_argument("--variant", default=None, help="K,red (one variant only)")
     a = ap.parse_args()
-    res = {"simple_200": run(200, 64, 5, 16), "simple_2000": run(2000, 40, 2, 3)}
+    global VARIANTS
+    if a.variant:
+        VARIANTS = [tuple(a.variant.split(","))]
+    cfg = {200: (64, 5, 16), 2000: (40, 2, 3), 2001: (100, 1, 3)}
+    res = {f"simple_{n}": run(min(n, 2000), *cfg.get(n, (40, 2, 3))) for n in a.frames}
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
 
