@@ -146,7 +146,7 @@ def main():
     print(json.dumps({"chen_2000": res["chen_2000"]}), flush=True)
     res["simple_200"] = simple_path(200, 64, 2 if q else 5, 64)
     print(json.dumps({"simple_200": res["simple_200"]}), flush=True)
-    res["simple_2000"] = simple_path(2000, 24, 1 if q else 2, 4)
+    res["simple_2000"] = simple_path(2000, 64, 1 if q else 2, 4)
     print(json.dumps({"simple_2000": res["simple_2000"]}), flush=True)
     with tempfile.TemporaryDirectory() as tmp:
         res["earlyfusion"] = earlyfusion_path(8 if q else 80, 20000, 4 if q else 8, tmp)
