@@ -16,7 +16,8 @@
 // reference;
 // window sums are sequential adds t = 0..L-1; dist = (sb[j] + sa[i]) - 2 qt.
 //
-// Fast path (L = 10, the reference's SSLEN; k_simple_diag<K>): one 256-thread block per pair.
+// Fast path (L = 10, the reference's SSLEN; k_simple_diag<K>, K = 5 by default): one 256-thread
+// block per pair (2 or 4 pairs per block for short tracks).
 // A wave owns 64·K consecutive diagonals o = j - i of the (P x Q) profile matrix, K adjacent
 // ones per lane, and walks down the rows: at step x every lane forms G(x, x + o) for its K
 // diagonals. The query frame x is wave-uniform (scalar loads); the K reference frames of a lane
@@ -452,11 +453,11 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
                      prof, fnorm, wnorm, ext, ldf);
   ACOSS_LAUNCH_CHECK();
   const char* kenv = getenv("ACOSS_SIMPLE_K");
-  const int kdiag = kenv ? atoi(kenv) : 4;
+  const int kdiag = kenv ? atoi(kenv) : 5;  // K = 5: 250 VGPRs, 2 waves per SIMD (measured fastest)
   const int n2max = pow2_at_least(max(max_len - kFastL + 1, 2));
   const int sboff = max(n2max, (int)max_len);  // the key buffer also holds nb frame norms first
   const int slotsz = sboff + (int)align_up((size_t)max_len, 2);
-  const int U = kdiag == 4 ? 20 : 10;
+  const int U = kdiag == 4 ? 20 : 10;  // lcm(10, K)
   // pairs per block: a block's 4 waves stay busy when a pair has fewer than 4 diagonal groups
   const int ngmax = (2 * max(max_len - kFastL + 1, 1) - 1 + 64 * kdiag - 1) / (64 * kdiag);
   const int ppb = ngmax <= 1 ? 4 : (ngmax <= 2 ? 2 : 1);
@@ -471,9 +472,10 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
     const int32_t* pp = pairs + 2 * p0;
     double* so = score_out + p0;
     int32_t* oo = oti_out ? oti_out + p0 : nullptr;
-    if (sslen == kFastL && (kdiag == 4 || kdiag == 2)) {
-      auto kern = kdiag == 4 ? (red ? k_simple_diag<4, 1> : k_simple_diag<4, 0>)
-                             : (red ? k_simple_diag<2, 1> : k_simple_diag<2, 0>);
+    if (sslen == kFastL && (kdiag == 5 || kdiag == 4 || kdiag == 2)) {
+      auto kern = kdiag == 5 ? k_simple_diag<5, 0>
+                  : kdiag == 4 ? (red ? k_simple_diag<4, 1> : k_simple_diag<4, 0>)
+                               : (red ? k_simple_diag<2, 1> : k_simple_diag<2, 0>);
       if (lds > 64 * 1024)
         ACOSS_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

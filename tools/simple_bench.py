@@ -20,7 +20,7 @@ from acoss import _lib  # noqa: E402
 import oracle  # noqa: E402
 
 
-VARIANTS = [("1", "1"), ("2", "0"), ("2", "1"), ("4", "0"), ("4", "1")]
+VARIANTS = [("2", "0"), ("4", "0"), ("4", "1"), ("5", "0")]
 
 
 def run(n, n_tracks, reps, check):
