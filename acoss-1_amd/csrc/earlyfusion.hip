@@ -98,8 +98,10 @@ template <int KIND>  // 0 euclid, 1 cosine (pre-normalised rows, query blocks ro
 __global__ __launch_bounds__(256) void k_ef_csm(const float* __restrict__ bank, int d, const float* __restrict__ sq,
                                                 EfPairs E, const int* __restrict__ oti, int ld,
                                                 float* __restrict__ out) {
-  __shared__ float Xs[kT][kKC + 1];
-  __shared__ float Ys[kT][kKC + 1];
+  // two LDS buffers: the next K chunk is loaded into registers while the MFMAs read this one,
+  // then stored to the other buffer; one barrier per chunk
+  __shared__ float Xs[2][kT][kKC + 1];
+  __shared__ float Ys[2][kT][kKC + 1];
   const int p = blockIdx.z;
   int a, b, M, N;
   pair_dims(E, p, &a, &b, &M, &N);
@@ -110,27 +112,48 @@ __global__ __launch_bounds__(256) void k_ef_csm(const float* __restrict__ bank, 
   const int roll = KIND == 1 ? oti[p] : 0;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wr = w >> 1, wc = w & 1;
-  f32x16 acc = {};
-  for (int k0 = 0; k0 < d; k0 += kKC) {
-    __syncthreads();
-    for (int e = t; e < kT * kKC; e += 256) {
-      const int r = e / kKC, c = e - r * kKC;
-      const int k = k0 + c;
-      int kx = k;
-      if (KIND == 1 && roll) {  // X1 = np.roll(X blocks, oti, axis=2): X1[k] = X[blk*12 + (cc - oti) mod 12]
-        const int blk = k / 12, cc = k - blk * 12;
-        kx = blk * 12 + (cc - roll + 12) % 12;
-      }
-      Xs[r][c] = (bi + r < M && k < d) ? X[(size_t)(bi + r) * d + kx] : 0.0f;
-      Ys[r][c] = (bj + r < N && k < d) ? Y[(size_t)(bj + r) * d + k] : 0.0f;
+  // loader: per load i, lane t reads row t / 32 + 8 i, k = k0 + t % 32 (32 lanes = one 128-B run)
+  constexpr int kPer = kT * kKC / 256;
+  const int lc = t % kKC, lr0 = t / kKC;
+  float xr[kPer], yr[kPer];
+  auto gload = [&](int k0) {
+    const int k = k0 + lc;
+    int kx = k;
+    if (KIND == 1 && roll) {  // X1 = np.roll(X blocks, oti, axis=2): X1[k] = X[blk*12 + (cc - oti) mod 12]
+      const int blk = k / 12, cc = k - blk * 12;
+      kx = blk * 12 + (cc - roll + 12) % 12;
     }
-    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int r = lr0 + (256 / kKC) * i;
+      xr[i] = (bi + r < M && k < d) ? X[(size_t)(bi + r) * d + kx] : 0.0f;
+      yr[i] = (bj + r < N && k < d) ? Y[(size_t)(bj + r) * d + k] : 0.0f;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      Xs[buf][lr0 + (256 / kKC) * i][lc] = xr[i];
+      Ys[buf][lr0 + (256 / kKC) * i][lc] = yr[i];
+    }
+  };
+  f32x16 acc = {};
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < d; k0 += kKC) {
+    const bool more = k0 + kKC < d;
+    if (more) gload(k0 + kKC);
 #pragma unroll
     for (int kk = 0; kk < kKC; kk += 2) {
-      const float xa = Xs[32 * wr + (lane & 31)][kk + (lane >> 5)];
-      const float yb = Ys[32 * wc + (lane & 31)][kk + (lane >> 5)];
+      const float xa = Xs[buf][32 * wr + (lane & 31)][kk + (lane >> 5)];
+      const float yb = Ys[buf][32 * wc + (lane & 31)][kk + (lane >> 5)];
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa, yb, acc, 0, 0, 0);
     }
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
   }
   float* o = out + (size_t)p * ld * ld;
   const int col = bj + 32 * wc + (lane & 31);
