@@ -11,9 +11,9 @@
 //                         rounding: parity with the reference is a tolerance, 1e-9 relative in the
 //                         tests; with the oracle's canonical order it is bit-exact).
 //
-// Canonical rounding (oracle/crp_oracle.cpp or_simple_sim): frame dot products and frame norms
-// are the product of bin 0 and then an fma chain over bins 1..11, of the query and of the ROLLED
-// reference;
+// Canonical rounding (oracle/crp_oracle.cpp or_simple_sim): the frame dot <a, roll(b, k)> runs
+// over the reference's own bins j = 0..11 paired with the query's bin (j + k) mod 12 (the
+// product for j = 0, then an fma chain); frame norms likewise over bins 0..11;
 // window sums are sequential adds t = 0..L-1; dist = (sb[j] + sa[i]) - 2 qt.
 //
 // Fast path (L = 10, the reference's SSLEN; k_simple_diag<K>, K = 5 by default): one 256-thread
@@ -21,13 +21,13 @@
 // A wave owns 64·K consecutive diagonals o = j - i of the (P x Q) profile matrix, K adjacent
 // ones per lane, and walks down the rows: at step x every lane forms G(x, x + o) for its K
 // diagonals. The query frame x is wave-uniform (scalar loads); the K reference frames of a lane
-// are consecutive columns, so each step loads ONE new frame per lane and rotates the others (the
-// ring index is static after unrolling by lcm(10, K)). Each diagonal keeps its 10 open window
+// are consecutive columns, so each step loads ONE new frame per lane (one aligned 128-B record)
+// and rotates the others (the ring index is static after unrolling by lcm(10, K)). Each diagonal keeps its 10 open window
 // partials in registers (slot = start step mod 10), so every G is formed once and added into the
 // windows in the canonical order. All cells completed at step x lie in row x - 9: one DPP wave
-// minimum per step, one LDS atomic per row per wave. Frames live in a per-track frame-major
-// copy with the 12 bins stored twice, so the rolled reference frame is 12 contiguous doubles at
-// bin offset (12 - k) mod 12. The median is a bitonic sort of the row minima in LDS.
+// minimum per step, one LDS atomic per row per wave. Per track: a frame-major query copy with
+// the 12 bins stored twice (the OTI pairing is the scalar load at bin offset k) and a reference
+// copy of 128-B records (12 bins + 4 pad). The median is a bitonic sort of the row minima in LDS.
 #include "common.hpp"
 
 namespace acoss {
@@ -37,7 +37,8 @@ namespace {
 constexpr int kMaxL = 16;
 constexpr int kMaxLen = 4096;  // frames per track (LDS: row minima + reference window norms)
 constexpr int kFastL = 10;     // simple_silva.py SSLEN
-constexpr int kExt = 24;       // doubles per frame in the frame-major copy (bins 0..11 twice)
+constexpr int kExt = 24;       // doubles per frame in the query copy (bins 0..11 twice)
+constexpr int kRec = 16;       // doubles per frame in the reference copy (bins 0..11 + pad: 128 B)
 
 __device__ __forceinline__ unsigned long long dkey(double v) {
   const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
@@ -68,7 +69,7 @@ __device__ int simple_oti_index(const double* pa, const double* pb) {
 __global__ void k_simple_track(const double* __restrict__ feats, const int64_t* __restrict__ off,
                                const int32_t* __restrict__ len, int n_tracks, int L, double* __restrict__ prof,
                                double* __restrict__ fnorm, double* __restrict__ wnorm, double* __restrict__ ext,
-                               int64_t ldf) {
+                               double* __restrict__ rec, int64_t ldf) {
   const int tr = blockIdx.x;
   if (tr >= n_tracks) return;
   const double* S = feats + off[tr];
@@ -80,6 +81,7 @@ __global__ void k_simple_track(const double* __restrict__ feats, const int64_t* 
     prof[tr * 12 + t] = acc;
   }
   double* E = ext + (size_t)tr * ldf * kExt;
+  double* R = rec + (size_t)tr * ldf * kRec;
   for (int x = t; x < n; x += blockDim.x) {
     double acc = 0.0;
     for (int d = 0; d < 12; ++d) {
@@ -87,7 +89,9 @@ __global__ void k_simple_track(const double* __restrict__ feats, const int64_t* 
       acc = d == 0 ? v * v : fma(v, v, acc);
       E[(size_t)x * kExt + d] = v;
       E[(size_t)x * kExt + 12 + d] = v;
+      R[(size_t)x * kRec + d] = v;
     }
+    for (int d = 12; d < kRec; ++d) R[(size_t)x * kRec + d] = 0.0;
     fnorm[(size_t)tr * ldf + x] = acc;
   }
   __syncthreads();
@@ -131,23 +135,10 @@ __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ 
   }
   __syncthreads();
   const int k = s_k;
-  int rowB[12];  // rolled reference: Brot[c] = B[(c - k) mod 12]
+  int rowA[12];  // reference bin j pairs with query bin (j + k) mod 12
 #pragma unroll
-  for (int c = 0; c < 12; ++c) rowB[c] = ((c - k + 12) % 12) * nb;
-  // reference window norms in the rolled bin order (the oracle sums Brot's bins 0..11)
-  for (int j = t; j < Q; j += 256) {
-    double acc = 0.0;
-    for (int u = 0; u < L; ++u) {
-      double f = B[rowB[0] + j + u] * B[rowB[0] + j + u];
-#pragma unroll
-      for (int c = 1; c < 12; ++c) {
-        const double v = B[rowB[c] + j + u];
-        f = fma(v, v, f);
-      }
-      acc = acc + f;
-    }
-    sb[j] = acc;
-  }
+  for (int c = 0; c < 12; ++c) rowA[c] = ((c + k) % 12) * na;
+  for (int j = t; j < Q; j += 256) sb[j] = wnorm[(size_t)tb * ldf + j];  // a roll keeps the norms
   __syncthreads();
   for (int dg = t; dg < P + Q - 1; dg += 256) {
     const int o = dg - (P - 1);  // j - i
@@ -158,9 +149,9 @@ __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ 
     for (int u = 0; u < kMaxL; ++u) buf[u] = 0.0;
     for (int x = r0; x <= r1 + L - 1; ++x) {
       const int y = x + o;
-      double g = A[x] * B[rowB[0] + y];
+      double g = A[rowA[0] + x] * B[y];
 #pragma unroll
-      for (int c = 1; c < 12; ++c) g = fma(A[(size_t)c * na + x], B[rowB[c] + y], g);
+      for (int c = 1; c < 12; ++c) g = fma(A[rowA[c] + x], B[(size_t)c * nb + y], g);
 #pragma unroll
       for (int u = 0; u < kMaxL - 1; ++u) buf[u] = buf[u + 1];
       buf[kMaxL - 1] = g;
@@ -239,7 +230,7 @@ constexpr int gcd_c(int a, int b) { return b == 0 ? a : gcd_c(b, a % b); }
 constexpr int kRbufStride = 72;  // doubles per rbuf row: 64 lanes + pad (+inf) for the segments
 
 template <int K, int RED>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_simple_diag(const double* __restrict__ ext, const int32_t* __restrict__ len,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_simple_diag(const double* __restrict__ ext, const double* __restrict__ rec, const int32_t* __restrict__ len,
                                                      const int32_t* __restrict__ pairs, const double* __restrict__ prof,
                                                      const double* __restrict__ wnorm, int64_t ldf, int n2max,
                                                      int sboff, int slotsz, int rboff, int ppb, int64_t n_pairs,
@@ -269,29 +260,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     if (!live) score[p] = __builtin_nan("");
   }
   __syncthreads();
-  const int shift = live ? __builtin_amdgcn_readfirstlane((12 - s_k[slot]) % 12) : 0;  // Brot[c] = ext[y][shift + c]
-  const double* Ea = ext + (size_t)ta * ldf * kExt;
-  const double* Eb = ext + (size_t)tb * ldf * kExt + shift;
+  const int kq = live ? __builtin_amdgcn_readfirstlane(s_k[slot]) : 0;  // query bin offset of the OTI pairing
+  const double* Ea = ext + (size_t)ta * ldf * kExt + kq;
+  const double* Eb = rec + (size_t)tb * ldf * kRec;
   const double* Wa = wnorm + (size_t)ta * ldf;
-  // rolled reference frame norms (fma chain over Brot's bins 0..11) into the key buffer, then
-  // the window sums into sb
-  double* fn = reinterpret_cast<double*>(mpk);
-  for (int y = tl; live && y < nb; y += nthr) {
-    double acc = Eb[(size_t)y * kExt] * Eb[(size_t)y * kExt];
-#pragma unroll
-    for (int c = 1; c < 12; ++c) {
-      const double v = Eb[(size_t)y * kExt + c];
-      acc = fma(v, v, acc);
-    }
-    fn[y] = acc;
-  }
-  __syncthreads();
-  for (int j = tl; live && j < Q; j += nthr) {
-    double acc = fn[j];
-#pragma unroll
-    for (int u = 1; u < L; ++u) acc = acc + fn[j + u];
-    sb[j] = acc;
-  }
+  // the reference's window norms (a roll keeps them) into LDS
+  for (int j = tl; live && j < Q; j += nthr) sb[j] = wnorm[(size_t)tb * ldf + j];
   __syncthreads();
   const int n2 = n2max;
   for (int i = tl; i < n2; i += nthr) mpk[i] = ~0ull;
@@ -319,7 +293,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     double part[K][L];
     auto load_frame = [&](int slot, int y) {
       const int yc = min(max(y, 0), nb - 1);
-      const double* src = Eb + (size_t)yc * kExt;
+      const double* src = Eb + (size_t)yc * kRec;
 #pragma unroll
       for (int c = 0; c < 12; ++c) F[slot][c] = src[c];
       const int cc = y - (L - 1);  // the cell column this frame closes
@@ -442,20 +416,22 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
   const int64_t ldf = (int64_t)align_up((size_t)max(max_len, 1), 64);
   const size_t prof_bytes = align_up((size_t)n_tracks * 12 * 8, 256);
   const size_t vec_bytes = (size_t)n_tracks * ldf * 8;
-  const size_t bytes = prof_bytes + 2 * vec_bytes + vec_bytes * kExt;
+  // vec_bytes is a multiple of 512 (ldf % 64 == 0): every section stays 128-B aligned
+  const size_t bytes = prof_bytes + 2 * vec_bytes + vec_bytes * kExt + vec_bytes * kRec;
   char* ws = static_cast<char*>(workspace(8, bytes));
   if (!ws) return ACOSS_E_HIP;
   double* prof = reinterpret_cast<double*>(ws);
   double* fnorm = reinterpret_cast<double*>(ws + prof_bytes);
   double* wnorm = reinterpret_cast<double*>(ws + prof_bytes + vec_bytes);
   double* ext = reinterpret_cast<double*>(ws + prof_bytes + 2 * vec_bytes);
+  double* rec = reinterpret_cast<double*>(ws + prof_bytes + 2 * vec_bytes + vec_bytes * kExt);
   hipLaunchKernelGGL(k_simple_track, dim3(n_tracks), dim3(256), 0, s, feats, track_off, track_len, n_tracks, sslen,
-                     prof, fnorm, wnorm, ext, ldf);
+                     prof, fnorm, wnorm, ext, rec, ldf);
   ACOSS_LAUNCH_CHECK();
   const char* kenv = getenv("ACOSS_SIMPLE_K");
   const int kdiag = kenv ? atoi(kenv) : 5;  // K = 5: 250 VGPRs, 2 waves per SIMD (measured fastest)
   const int n2max = pow2_at_least(max(max_len - kFastL + 1, 2));
-  const int sboff = max(n2max, (int)max_len);  // the key buffer also holds nb frame norms first
+  const int sboff = n2max;
   const int slotsz = sboff + (int)align_up((size_t)max_len, 2);
   const int U = kdiag == 4 ? 20 : 10;  // lcm(10, K)
   // pairs per block: a block's 4 waves stay busy when a pair has fewer than 4 diagonal groups
@@ -479,7 +455,7 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
       if (lds > 64 * 1024)
         ACOSS_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(kern, dim3((unsigned)((np + ppb - 1) / ppb)), dim3(256), lds, s, ext, track_len, pp, prof,
+      hipLaunchKernelGGL(kern, dim3((unsigned)((np + ppb - 1) / ppb)), dim3(256), lds, s, ext, rec, track_len, pp, prof,
                          wnorm, ldf, n2max, sboff, slotsz, rboff, ppb, np, apply_oti, so, oo);
     } else {
       hipLaunchKernelGGL(k_simple_pair, dim3((unsigned)np), dim3(256), 0, s, feats, track_off, track_len, pp, prof,

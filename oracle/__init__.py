@@ -56,7 +56,7 @@ def lib():
         L.or_sw_constrained.restype = ctypes.c_double
         L.or_sw_constrained.argtypes = [_u8p, ctypes.c_int, ctypes.c_int]
         L.or_simple_sim.restype = ctypes.c_double
-        L.or_simple_sim.argtypes = [_dp, ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int]
+        L.or_simple_sim.argtypes = [_dp, ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.or_track_profile.argtypes = [_fp, ctypes.c_int, _fp]
         L.or_oti.argtypes = [_fp, _fp]
         L.or_simple_oti.restype = ctypes.c_int
@@ -129,10 +129,12 @@ def sw_constrained(B):
     return float(lib().or_sw_constrained(_p(B, _u8p), B.shape[0], B.shape[1]))
 
 
-def simple_sim(A, B, sslen=10):
+def simple_sim(A, B, sslen=10, k=0):
+    """Simple.simple_sim of query A against the reference B rolled by k on the chroma axis
+    (simple_silva.py:45-118; k = the Simple.oti index, 0 = no roll). (12, n) float64 blocks."""
     A = np.ascontiguousarray(A, np.float64)
     B = np.ascontiguousarray(B, np.float64)
-    return float(lib().or_simple_sim(_p(A, _dp), A.shape[1], _p(B, _dp), B.shape[1], sslen))
+    return float(lib().or_simple_sim(_p(A, _dp), A.shape[1], _p(B, _dp), B.shape[1], int(k), sslen))
 
 
 def profile(X):

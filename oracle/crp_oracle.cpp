@@ -279,18 +279,21 @@ double or_sw_constrained(const uint8_t* B, int M, int N) {
 }
 
 // acoss Simple.simple_sim (simple_silva.py:68-118): median over i of
-// min_j ||A[:, i:i+L] - B[:, j:j+L]||^2 computed as sa + sb - 2 QT (float64). Canonical order
-// (shared with simple.hip): frame dots and frame norms are a product of bin 0 then an fma chain over bins 1..11,
-// window sums are sequential adds.
-// A: 12 x na, B: 12 x nb, both row-major (dim-major) as in the reference.
-double or_simple_sim(const double* A, int na, const double* B, int nb, int L) {
+// min_j ||A[:, i:i+L] - Brot[:, j:j+L]||^2 computed as sa + sb - 2 QT (float64), where Brot is
+// the reference rolled by k on the chroma axis (Simple.oti, :45-54). Canonical order (shared
+// with simple.hip): the frame dot <A[:, x], Brot[:, y]> runs over the reference's OWN bins
+// j = 0..11 paired with the query's bin (j + k) mod 12 -- the product for j = 0, then an fma
+// chain; frame norms likewise over bins 0..11 (a roll does not change them); window sums are
+// sequential adds.
+double or_simple_sim(const double* A, int na, const double* B, int nb, int k, int L) {
   const int P = na - L + 1, Q = nb - L + 1;
   if (P <= 0 || Q <= 0) return NAN;
+  k = ((k % 12) + 12) % 12;
   std::vector<double> ga((size_t)na * nb);
   for (int x = 0; x < na; ++x)
     for (int y = 0; y < nb; ++y) {
-      double acc = A[x] * B[y];
-      for (int d = 1; d < 12; ++d) acc = std::fma(A[(size_t)d * na + x], B[(size_t)d * nb + y], acc);
+      double acc = A[(size_t)(k % 12) * na + x] * B[y];
+      for (int d = 1; d < 12; ++d) acc = std::fma(A[(size_t)((d + k) % 12) * na + x], B[(size_t)d * nb + y], acc);
       ga[(size_t)x * nb + y] = acc;
     }
   std::vector<double> na2(na), nb2(nb), sa(P), sb(Q), mp(P);

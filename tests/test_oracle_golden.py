@@ -65,6 +65,8 @@ def test_oracle_simple_golden(gold, tag):
     np.testing.assert_array_equal(np.roll(B, k, axis=0), gold[tag + "_Brot"])
     Brot, k2 = npo.simple_oti(A, B)
     assert k2 == k
+    np.testing.assert_allclose(oracle.simple_sim(A, B, k=k), float(gold[tag + "_score"]), rtol=1e-12)
+    # the same restatement on the pre-rolled reference (k = 0) sums in another bin order
     np.testing.assert_allclose(oracle.simple_sim(A, Brot), float(gold[tag + "_score"]), rtol=1e-12)
 
 
