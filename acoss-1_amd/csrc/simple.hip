@@ -229,7 +229,18 @@ constexpr int gcd_c(int a, int b) { return b == 0 ? a : gcd_c(b, a % b); }
 // per row each fold a 16-B aligned segment of that row and ds_min the key (at most S-way).
 constexpr int kRbufStride = 72;  // doubles per rbuf row: 64 lanes + pad (+inf) for the segments
 
-template <int K, int RED>
+// Lane l gets lane l + 1's double; lane 63 keeps `old` (DPP wave_shl:1, bound_ctrl off).
+__device__ __forceinline__ double dpp_shl1_f64(double old, double v) {
+  const unsigned long long o = __builtin_bit_cast(unsigned long long, old);
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = dpp_u32<0x130, 0xf>((unsigned)o, (unsigned)u);
+  const unsigned hi = dpp_u32<0x130, 0xf>((unsigned)(o >> 32), (unsigned)(u >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// SH = 1: a lane's new reference frame is the frame lane l + 1 drops this step (DPP), so the
+// wave reads ONE frame per step (lane 63's, a wave-uniform address loaded a step ahead).
+template <int K, int RED, int SH = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_simple_diag(const double* __restrict__ ext, const double* __restrict__ rec, const int32_t* __restrict__ len,
                                                      const int32_t* __restrict__ pairs, const double* __restrict__ prof,
                                                      const double* __restrict__ wnorm, int64_t ldf, int n2max,
@@ -301,6 +312,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     };
 #pragma unroll
     for (int k = 0; k < K - 1; ++k) load_frame(k, xs + yl + k);
+    double PF[12], PFsb = 0.0;  // SH: lane 63's next frame (wave-uniform column)
+    auto load_pf = [&](int y) {
+      const int yc = min(max(y, 0), nb - 1);
+      const double* src = Eb + (size_t)yc * kRec;
+#pragma unroll
+      for (int c = 0; c < 12; ++c) PF[c] = src[c];
+      const int cc = y - (L - 1);
+      PFsb = (cc >= 0 && cc < Q) ? sb[cc] : kInf;
+    };
+    if (SH) {
+      load_frame(K - 1, xs - 1 + yl);  // what lane l - 1 takes over at the first step
+      load_pf(xs + ob + 64 * K - 1);
+    }
 #pragma unroll
     for (int k = 0; k < K; ++k)
 #pragma unroll
@@ -309,7 +333,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
       for (int ph = 0; ph < U; ++ph) {
         const int x = x0 + ph;
-        load_frame((ph + K - 1) % K, x + yl + K - 1);
+        if (SH) {
+          const int sl = (ph + K - 1) % K;
+#pragma unroll
+          for (int c = 0; c < 12; ++c) F[sl][c] = dpp_shl1_f64(PF[c], F[sl][c]);
+          SB[sl] = dpp_shl1_f64(PFsb, SB[sl]);
+          load_pf(x + 1 + ob + 64 * K - 1);
+        } else {
+          load_frame((ph + K - 1) % K, x + yl + K - 1);
+        }
         // wave-uniform query frame and window norm: scalar loads (constant address space)
         const CDouble* Arow = (const CDouble*)(Ea + (size_t)min(x, na - 1) * kExt);
         double a[12];
@@ -429,7 +461,9 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
                      prof, fnorm, wnorm, ext, rec, ldf);
   ACOSS_LAUNCH_CHECK();
   const char* kenv = getenv("ACOSS_SIMPLE_K");
-  const int kdiag = kenv ? atoi(kenv) : 5;  // K = 5: 250 VGPRs, 2 waves per SIMD (measured fastest)
+  // K = 4 with DPP frame passing for long tracks (2000 frames: 133.5k pairs/s vs 101.3k for K = 5
+  // loading every frame), K = 5 for short ones (200 frames: 5.27M vs 5.11M)
+  const int kdiag = kenv ? atoi(kenv) : (max_len >= 512 ? 4 : 5);
   const int n2max = pow2_at_least(max(max_len - kFastL + 1, 2));
   const int sboff = n2max;
   const int slotsz = sboff + (int)align_up((size_t)max_len, 2);
@@ -448,8 +482,11 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
     const int32_t* pp = pairs + 2 * p0;
     double* so = score_out + p0;
     int32_t* oo = oti_out ? oti_out + p0 : nullptr;
-    if (sslen == kFastL && (kdiag == 5 || kdiag == 4 || kdiag == 2)) {
-      auto kern = kdiag == 5 ? k_simple_diag<5, 0>
+    if (sslen == kFastL && (kdiag == 2 || kdiag == 4 || kdiag == 5)) {
+      const char* senv = getenv("ACOSS_SIMPLE_SH");
+      const int sh = senv ? atoi(senv) : 1;
+      auto kern = (kdiag == 4 && sh) ? k_simple_diag<4, 0, 1>
+                  : kdiag == 5 ? k_simple_diag<5, 0>
                   : kdiag == 4 ? (red ? k_simple_diag<4, 1> : k_simple_diag<4, 0>)
                                : (red ? k_simple_diag<2, 1> : k_simple_diag<2, 0>);
       if (lds > 64 * 1024)

@@ -190,9 +190,9 @@ def test_simple_batch_vs_oracle(lib):
         assert score[p] == ref or (np.isnan(ref) and np.isnan(score[p]))
 
 
-@pytest.mark.parametrize("sslen,kdiag", [(10, None), (10, "2"), (10, "4"), (7, None)])
+@pytest.mark.parametrize("sslen,kdiag", [(10, None), (10, "2"), (10, "4"), (10, "5"), (7, None)])
 def test_simple_long_vs_oracle(lib, monkeypatch, sslen, kdiag):
-    """Fast diagonal kernel (L = 10, K = 2 / 4 diagonals per lane) and the generic sslen path on
+    """Fast diagonal kernel (L = 10, K = 2 / 4 / 5 diagonals per lane; K = 4 passes frames by DPP) and the generic sslen path on
     tracks up to 1300 frames with unequal lengths (ragged diagonal groups), bit-exact."""
     if kdiag is not None:
         monkeypatch.setenv("ACOSS_SIMPLE_K", kdiag)
@@ -212,3 +212,21 @@ def test_simple_long_vs_oracle(lib, monkeypatch, sslen, kdiag):
         assert oti[p] == k
         ref = oracle.simple_sim(feats[i], feats[j], sslen, k=k)
         assert score[p] == ref or (np.isnan(ref) and np.isnan(score[p])), (i, j, score[p], ref)
+
+
+def test_simple_max_length_vs_oracle(lib):
+    """A 4096-frame track (the ABI's maximum: 64 KB of per-pair LDS) against a short one, both
+    directions, plus the short track against itself (zero distances); bit-exact against the oracle."""
+    rng = np.random.default_rng(4096)
+    feats = []
+    for n in [4096, 350]:
+        F = np.abs(rng.standard_normal((12, n)))
+        F /= np.linalg.norm(F, axis=0, keepdims=True)
+        feats.append(F)
+    pairs = np.array([(0, 1), (1, 0), (1, 1)], dtype=np.int32)
+    score, oti = lib.simple_mp(feats, pairs)
+    score, oti = _np(score), _np(oti)
+    for p, (i, j) in enumerate(pairs):
+        k = oracle.simple_oti(feats[i], feats[j])
+        assert oti[p] == k
+        assert score[p] == oracle.simple_sim(feats[i], feats[j], 10, k=k), (i, j)

@@ -20,7 +20,7 @@ from acoss import _lib  # noqa: E402
 import oracle  # noqa: E402
 
 
-VARIANTS = [("2", "0"), ("4", "0"), ("4", "1"), ("5", "0")]
+VARIANTS = [("5", "0", "0"), ("4", "0", "1")]
 
 
 def run(n, n_tracks, reps, check):
@@ -39,8 +39,11 @@ def run(n, n_tracks, reps, check):
         k = oracle.simple_oti(feats[i], feats[j])
         ref.append(oracle.simple_sim(feats[i], feats[j], k=k))
     out = {}
-    for kd, red in VARIANTS:
+    for v in VARIANTS:
+        kd, red = v[0], v[1]
         os.environ["ACOSS_SIMPLE_RED"] = red
+        os.environ["ACOSS_SIMPLE_SH"] = v[2] if len(v) > 2 else "0"
+        red = red + ("s" + v[2] if len(v) > 2 else "")
         os.environ["ACOSS_SIMPLE_K"] = kd
         score, _ = _lib.simple_mp_packed(flat, off, lens, pt)
         torch.cuda.synchronize()
