@@ -21,8 +21,10 @@
 // A wave owns 64·K consecutive diagonals o = j - i of the (P x Q) profile matrix, K adjacent
 // ones per lane, and walks down the rows: at step x every lane forms G(x, x + o) for its K
 // diagonals. The query frame x is wave-uniform (scalar loads); the K reference frames of a lane
-// are consecutive columns, so each step loads ONE new frame per lane (one aligned 128-B record)
-// and rotates the others (the ring index is static after unrolling by lcm(10, K)). Each diagonal keeps its 10 open window
+// are consecutive columns, so each step needs ONE new frame per lane (one aligned 128-B record)
+// and rotates the others (the ring index is static after unrolling by lcm(10, K)). With SH (the
+// default for tracks of >= 512 frames, K = 4) that frame is the one lane l + 1 drops this step:
+// a DPP wave_shl:1 hands it over and only lane 63's frame, a wave-uniform column, is loaded. Each diagonal keeps its 10 open window
 // partials in registers (slot = start step mod 10), so every G is formed once and added into the
 // windows in the canonical order. All cells completed at step x lie in row x - 9: one DPP wave
 // minimum per step, one LDS atomic per row per wave. Per track: a frame-major query copy with
