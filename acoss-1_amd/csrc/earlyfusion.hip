@@ -310,9 +310,10 @@ __global__ __launch_bounds__(256) void k_ef_kmean(const float* __restrict__ C, i
 // min/max inserts the rest). Columns: lanes read consecutive columns (coalesced); rows: each
 // lane walks its own row (cache lines reused along the walk). Sum in ascending order (the
 // reference's np.mean over np.partition output has unspecified order: tolerance).
-template <bool COLS, int KMAX>
+template <bool COLS, int KMAX, int KC = 0>  // KC > 0: k fixed at compile time (k = KC = KMAX)
 __global__ __launch_bounds__(256) void k_ef_kmin(const float* __restrict__ C, int64_t mat_stride, int ld, EfPairs E,
-                                                 int k, float* __restrict__ out, int64_t omat_stride) {
+                                                 int k_rt, float* __restrict__ out, int64_t omat_stride) {
+  const int k = KC ? KC : k_rt;
   const int p = blockIdx.y, m = blockIdx.z;
   int a, b, M, N;
   pair_dims(E, p, &a, &b, &M, &N);
@@ -350,10 +351,11 @@ __global__ __launch_bounds__(256) void k_ef_kmin(const float* __restrict__ C, in
 // Row variant of k_ef_kmin: a wave takes 64 rows and stages 64 x 64 tiles through LDS with
 // coalesced row-segment loads; lane r then walks row r of the tile (same insertion order as
 // k_ef_kmin<false>: columns ascending).
-template <int KMAX>
+template <int KMAX, int KC = 0>
 __global__ __launch_bounds__(64) void k_ef_kmin_rows(const float* __restrict__ C, int64_t mat_stride, int ld,
-                                                     EfPairs E, int k, float* __restrict__ out,
+                                                     EfPairs E, int k_rt, float* __restrict__ out,
                                                      int64_t omat_stride) {
+  const int k = KC ? KC : k_rt;
   __shared__ float t[64][65];
   const int p = blockIdx.y, m = blockIdx.z;
   int a, b, M, N;
@@ -528,7 +530,14 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_BIN, s);
     prof_begin(PH_WCSM, s);
-    if (K <= kKmax) {
+    if (K == 10) {  // EarlyFusion's K: the k-th smallest is a fixed register, no per-element select
+      hipLaunchKernelGGL((k_ef_kmin_rows<10, 10>), dim3((ld + 63) / 64, P, 3), dim3(64), 0, s, C, mstride, ld, E,
+                         (int)K, rmean, meanstride);
+      ACOSS_LAUNCH_CHECK();
+      hipLaunchKernelGGL((k_ef_kmin<true, 10, 10>), dim3((ld + 255) / 256, P, 3), dim3(256), 0, s, C, mstride, ld,
+                         E, (int)K, cmean, meanstride);
+      ACOSS_LAUNCH_CHECK();
+    } else if (K <= kKmax) {
       hipLaunchKernelGGL((k_ef_kmin_rows<kKmax>), dim3((ld + 63) / 64, P, 3), dim3(64), 0, s, C, mstride, ld, E,
                          (int)K, rmean, meanstride);
       ACOSS_LAUNCH_CHECK();
