@@ -178,6 +178,7 @@ __global__ __launch_bounds__(256) void k_ef_csm(const float* __restrict__ bank, 
 // takes 16 rows (one wave per row) and writes them as one row of u16 bit words (bit r = row
 // 16g + r) in LDS, then to the pair's bit plane for SW. blockIdx.z = CSM plane, written to
 // bit plane z + plane0 of the pair (plane stride = wplane words, 4 planes per pair).
+template <int KB>  // keys per lane held in registers (rows of up to 64 * KB columns)
 __device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int N, double kappa, int lane,
                                                 unsigned* bits, unsigned bit) {
   if (kappa == 0.0) {
@@ -189,13 +190,13 @@ __device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int
   const int per = (N + 63) / 64;
   const int c0 = lane * per, c1 = min(N, c0 + per);
   unsigned lo = 0, hi = 0xffffffffu;
-  if (per <= kBinRegs) {  // the row's keys in registers: one pass over memory
-    unsigned kr[kBinRegs];
+  if (per <= KB) {  // the row's keys in registers: one pass over memory
+    unsigned kr[KB];
 #pragma unroll
-    for (int q = 0; q < kBinRegs; ++q) kr[q] = (q < per && c0 + q < c1) ? fkey(x[c0 + q]) : 0xffffffffu;
+    for (int q = 0; q < KB; ++q) kr[q] = (q < per && c0 + q < c1) ? fkey(x[c0 + q]) : 0xffffffffu;
     unsigned mn = 0xffffffffu, mx = 0u;  // bound the search by the row's range
 #pragma unroll
-    for (int q = 0; q < kBinRegs; ++q) {
+    for (int q = 0; q < KB; ++q) {
       mn = min(mn, kr[q]);
       if (q < per && c0 + q < c1) mx = max(mx, kr[q]);
     }
@@ -205,7 +206,7 @@ __device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int
       const unsigned mid = lo + ((hi - lo) >> 1);
       int c = 0;
 #pragma unroll
-      for (int q = 0; q < kBinRegs; ++q) c += kr[q] <= mid;
+      for (int q = 0; q < KB; ++q) c += kr[q] <= mid;
       if (wave_sum(c) >= nn)
         hi = mid;
       else
@@ -254,8 +255,13 @@ __global__ __launch_bounds__(1024) void k_ef_binarize(const float* __restrict__ 
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = 16 * g + w;
-  if (row < M)
-    ef_binarize_row(C + m * mat_stride + (size_t)p * ld * ld + (size_t)row * ld, N, kappa, lane, bits, 1u << w);
+  if (row < M) {
+    const float* xr = C + m * mat_stride + (size_t)p * ld * ld + (size_t)row * ld;
+    if (N <= 64 * 8)  // EarlyFusion's ~450-block tracks: 8 key registers halve the count passes
+      ef_binarize_row<8>(xr, N, kappa, lane, bits, 1u << w);
+    else
+      ef_binarize_row<kBinRegs>(xr, N, kappa, lane, bits, 1u << w);
+  }
   __syncthreads();
   uint16_t* o = Wb + ((size_t)p * 4 + plane0 + m) * wplane + (size_t)g * ld;
   for (int c = threadIdx.x; c < N; c += 1024) o[c] = (uint16_t)bits[c];
