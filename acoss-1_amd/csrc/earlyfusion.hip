@@ -102,10 +102,14 @@ __global__ __launch_bounds__(256) void k_ef_csm(const float* __restrict__ bank, 
   // then stored to the other buffer; one barrier per chunk
   __shared__ float Xs[2][kT][kKC + 1];
   __shared__ float Ys[2][kT][kKC + 1];
-  const int p = blockIdx.z;
+  // 1-D grid of tiles x tiles x pairs, XCD-aware: the tiles of one pair run on one XCD, so its
+  // row and column panels are read into that XCD's L2 once and reused by the pair's other tiles
+  const int tiles = (ld + kT - 1) / kT;
+  const int lg = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int p = lg / (tiles * tiles), tix = lg - p * tiles * tiles;
   int a, b, M, N;
   pair_dims(E, p, &a, &b, &M, &N);
-  const int bi = blockIdx.y * kT, bj = blockIdx.x * kT;
+  const int bi = (tix / tiles) * kT, bj = (tix % tiles) * kT;
   if (bi >= M || bj >= N) return;
   const float* X = bank + E.off[a] * d;
   const float* Y = bank + E.off[b] * d;
@@ -521,12 +525,12 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
     prof_begin(PH_CSM, s);
     hipLaunchKernelGGL(k_ef_oti, dim3((P + 255) / 256), dim3(256), 0, s, chroma_med, pairs + 2 * p0, P, oti);
     ACOSS_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ef_csm<0>, dim3(tiles, tiles, P), dim3(256), 0, s, mfcc, d_mfcc, sq_m, E, oti, ld, C);
+    hipLaunchKernelGGL(k_ef_csm<0>, dim3((unsigned)(tiles * tiles * P)), dim3(256), 0, s, mfcc, d_mfcc, sq_m, E, oti, ld, C);
     ACOSS_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ef_csm<0>, dim3(tiles, tiles, P), dim3(256), 0, s, ssm, d_ssm, sq_s, E, oti, ld,
+    hipLaunchKernelGGL(k_ef_csm<0>, dim3((unsigned)(tiles * tiles * P)), dim3(256), 0, s, ssm, d_ssm, sq_s, E, oti, ld,
                        C + mstride);
     ACOSS_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ef_csm<1>, dim3(tiles, tiles, P), dim3(256), 0, s, chn, d_chroma, nullptr, E, oti, ld,
+    hipLaunchKernelGGL(k_ef_csm<1>, dim3((unsigned)(tiles * tiles * P)), dim3(256), 0, s, chn, d_chroma, nullptr, E, oti, ld,
                        C + 2 * mstride);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_CSM, s);
