@@ -472,7 +472,12 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
   const int U = kdiag == 4 ? 20 : 10;  // lcm(10, K)
   // pairs per block: a block's 4 waves stay busy when a pair has fewer than 4 diagonal groups
   const int ngmax = (2 * max(max_len - kFastL + 1, 1) - 1 + 64 * kdiag - 1) / (64 * kdiag);
-  const int ppb = ngmax <= 1 ? 4 : (ngmax <= 2 ? 2 : 1);
+  // a pair with at most 2 groups goes to ONE wave (it walks both: no wave of the block idles
+  // while its partner finishes the longer group; 200 frames: 6.02M vs 4.95M pairs/s with 2 waves)
+  const char* penv = getenv("ACOSS_SIMPLE_PPB");
+  int ppb = penv ? atoi(penv) : (ngmax <= 2 ? 4 : 1);
+  if (ppb != 1 && ppb != 2 && ppb != 4) ppb = 1;
+  while (ppb > 1 && (size_t)ppb * (n2max + align_up((size_t)max_len, 2)) * 8 > 96 * 1024) ppb /= 2;
   // row minima through LDS chunks for packed short pairs, per-step DPP minima for long ones
   // (measured: 200 frames 5.85M vs 5.58M pairs/s, 2000 frames 48.0k vs 51.0k)
   const char* renv = getenv("ACOSS_SIMPLE_RED");

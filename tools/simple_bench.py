@@ -20,7 +20,7 @@ from acoss import _lib  # noqa: E402
 import oracle  # noqa: E402
 
 
-VARIANTS = [("5", "0", "0"), ("4", "0", "1")]
+VARIANTS = [("5", "0", "0"), ("4", "0", "1")]  # (K, red, sh[, ppb])
 
 
 def run(n, n_tracks, reps, check):
@@ -43,7 +43,11 @@ def run(n, n_tracks, reps, check):
         kd, red = v[0], v[1]
         os.environ["ACOSS_SIMPLE_RED"] = red
         os.environ["ACOSS_SIMPLE_SH"] = v[2] if len(v) > 2 else "0"
-        red = red + ("s" + v[2] if len(v) > 2 else "")
+        if len(v) > 3:
+            os.environ["ACOSS_SIMPLE_PPB"] = v[3]
+        else:
+            os.environ.pop("ACOSS_SIMPLE_PPB", None)
+        red = red + ("s" + v[2] if len(v) > 2 else "") + ("p" + v[3] if len(v) > 3 else "")
         os.environ["ACOSS_SIMPLE_K"] = kd
         score, _ = _lib.simple_mp_packed(flat, off, lens, pt)
         torch.cuda.synchronize()
