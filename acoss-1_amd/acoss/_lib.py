@@ -50,6 +50,8 @@ SIGNATURES = {
     "acoss_simple_features": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _i64, _vp],
     "acoss_earlyfusion": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, ctypes.c_double,
                           _i32, _f32, _vp, _vp],
+    "acoss_ds_finish": [_vp, _i32, _i64, _vp, _i32, _i32, _vp, _vp],
+    "acoss_eval_ranks": [_vp, _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp],
     "acoss_release_workspace": [],
     "acoss_profile_enable": [ctypes.c_int],
     "acoss_profile_read": [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int],
@@ -443,6 +445,53 @@ def earlyfusion(bank, pairs, kappa=0.1, K=10, mu=0.5):
                                _ptr(pairs), int(P), float(kappa), int(K), float(mu), _ptr(out), _stream())
     _check(rc, "acoss_earlyfusion")
     return out
+
+
+FINISH_MODES = {None: 0, "none": 0, "serra09": 1, "chen": 2}
+
+
+def ds_finish(D, norm=None, symmetric=True, mode=None, out=None):
+    """acoss_ds_finish on a (n, n) float32 device matrix: Ds += Ds.T (symmetric) then the
+    Serra09 (D / sqrt(n_j)) or Chen (sqrt(n_j) / D) length normalisation with norm[j] =
+    sqrt(n_j) in float64. In place unless `out` is given."""
+    torch = _torch()
+    lib = load_library()
+    if D.dtype != torch.float32 or not D.is_cuda or D.dim() != 2 or D.shape[0] != D.shape[1] or D.stride(1) != 1:
+        raise ValueError("ds_finish takes a square float32 CUDA matrix with unit column stride")
+    m = FINISH_MODES[mode]
+    nrm = _dev(norm, torch.float64) if m else None
+    if m and nrm.numel() != D.shape[0]:
+        raise ValueError("norm must hold one factor per column")
+    out = D if out is None else out
+    if out.shape != D.shape or out.dtype != D.dtype or out.stride() != D.stride():
+        raise ValueError("out must match D")
+    rc = lib.acoss_ds_finish(_ptr(D), int(D.shape[0]), int(D.stride(0)), _ptr(nrm), int(bool(symmetric)), m,
+                             _ptr(out), _stream())
+    _check(rc, "acoss_ds_finish")
+    return out
+
+
+def eval_ranks(D, pos, q_song, m_off, members):
+    """acoss_eval_ranks: rank (1-based) of members[m_off[q]:m_off[q+1]] in row q_song[q] of D,
+    in np.argsort(-D', 1, kind='stable') order of the clique-permuted matrix (pos = each song's
+    position in that order), diagonal -inf. Returns an int32 numpy array."""
+    torch = _torch()
+    lib = load_library()
+    if D.dtype != torch.float32 or not D.is_cuda or D.stride(1) != 1:
+        raise ValueError("eval_ranks takes a float32 CUDA matrix with unit column stride")
+    n = int(D.shape[0])
+    pos = _dev(pos, torch.int32)
+    q_song = _dev(q_song, torch.int32)
+    m_off = _dev(m_off, torch.int64)
+    members = _dev(members, torch.int32)
+    for name, t in (("q_song", q_song), ("members", members)):
+        if t.numel() and (int(t.min()) < 0 or int(t.max()) >= n):
+            raise ValueError("%s must lie in [0, %d)" % (name, n))
+    out = torch.empty(members.numel(), dtype=torch.int32, device="cuda")
+    rc = lib.acoss_eval_ranks(_ptr(D), n, int(D.stride(0)), _ptr(pos), _ptr(q_song), _ptr(m_off), _ptr(members),
+                              int(q_song.numel()), _ptr(out), _stream())
+    _check(rc, "acoss_eval_ranks")
+    return out.cpu().numpy()
 
 
 def profile_enable(on=True):

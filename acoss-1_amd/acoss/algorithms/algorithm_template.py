@@ -14,8 +14,15 @@ What changes is how the pair loop runs (algorithm_template.py:142-193). The refe
   * with torch.distributed initialised (one process per GPU, RCCL), every rank scores one
     cost-balanced row stripe (acoss.distributed) and ONE all-gather assembles Ds on every
     rank; `parallel` / `n_cores` are accepted for signature compatibility and ignored;
-  * Ds is saved as '<prefix>_Ds.npz' (deepdish/h5py are absent; `precomputed=True` reads it
-    back, or the reference's '<prefix>_Ds.h5' when h5py is importable).
+  * subclasses with a HIP scorer (`_device_scores`) keep the stripe on the device: the
+    all-gather, `Ds += Ds.T` and the subclasses' normalize_by_length run as HIP kernels
+    (finish.hip), and getEvalStatistics ranks on the device (acoss_eval_ranks), so no O(N^2)
+    host loop is left for Da-TACOS-sized runs (SURVEY.md §8f row 1);
+  * only rank 0 keeps the file-backed memmap and writes the results (other ranks hold Ds in
+    memory), so ranks never write the same file;
+  * Ds is saved as '<prefix>_Ds.h5' (the reference's file, :163,193; one dataset per
+    similarity type, as deepdish lays out a dict) when h5py is importable, and always as the
+    '<prefix>_Ds.npz' twin; `precomputed=True` reads either back.
 Reference defects not reproduced: the NameError of parallel=True at
 :174-192 and `cleanup_memmap` calling rmtree on files (:202).
 """
@@ -44,6 +51,14 @@ def _dist_info():
     return 1, 0
 
 
+def _on_gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except ImportError:
+        return False
+
+
 class CoverAlgorithm(object):
     def __init__(self, dataset_csv, name="Serra09", datapath="features_benchmark", shortname="full",
                  cachedir="cache", similarity_types=["main"]):
@@ -55,9 +70,13 @@ class CoverAlgorithm(object):
         self.N = len(self.filepaths)
         os.makedirs(cachedir, exist_ok=True)
         self.Ds = {}
+        _, rank = _dist_info()
         for s in similarity_types:
-            self.Ds[s] = np.memmap("%s_%s_dmat" % (self.get_cacheprefix(), s), shape=(self.N, self.N), mode="w+",
-                                   dtype="float32")
+            if rank == 0:
+                self.Ds[s] = np.memmap("%s_%s_dmat" % (self.get_cacheprefix(), s), shape=(self.N, self.N),
+                                       mode="w+", dtype="float32")
+            else:
+                self.Ds[s] = np.zeros((self.N, self.N), np.float32)
         self._prepared = False
         print("Initialized %s algorithm on %i songs in dataset %s" % (name, self.N, shortname))
 
@@ -109,6 +128,11 @@ class CoverAlgorithm(object):
         for key in self.Ds:
             self.Ds[key][idxs[:, 0], idxs[:, 1]] = 0.0
 
+    def _device_scores(self, idxs):
+        """Subclasses with a HIP scorer return {similarity type: float32 CUDA tensor (P,)} for the
+        (P, 2) pairs; the base class has none (None: the host `similarity` loop is used)."""
+        return None
+
     def all_pairwise(self, parallel=0, n_cores=12, symmetric=False, precomputed=False):
         prefix = self.get_cacheprefix()
         if precomputed:
@@ -123,15 +147,38 @@ class CoverAlgorithm(object):
             bounds = [(0, self.N)]
         r0, r1 = bounds[rank]
         pairs = _dist.stripe_pairs(self.N, r0, r1, symmetric)
-        for c0 in range(0, len(pairs), PAIR_CHUNK):
-            self.similarity(pairs[c0:c0 + PAIR_CHUNK])
-        if world > 1:
-            self._gather_stripes(bounds, r0, r1)
-        if symmetric:
-            for key in self.Ds:
-                self.Ds[key] += self.Ds[key].T
+        if not self._device_all_pairwise(pairs, bounds, r0, r1, world, symmetric):
+            for c0 in range(0, len(pairs), PAIR_CHUNK):
+                self.similarity(pairs[c0:c0 + PAIR_CHUNK])
+            if world > 1:
+                self._gather_stripes(bounds, r0, r1)
+            if symmetric:
+                for key in self.Ds:
+                    self.Ds[key] += self.Ds[key].T
         if rank == 0:
             self._save_Ds(prefix)
+
+    def _device_all_pairwise(self, pairs, bounds, r0, r1, world, symmetric):
+        """The pair loop with the stripe kept in HBM: score chunks on the device, scatter into
+        the (r1 - r0, N) stripe, one all-gather (world > 1), symmetrise with acoss_ds_finish,
+        one copy into Ds. Returns False if the subclass has no device scorer."""
+        if type(self)._device_scores is CoverAlgorithm._device_scores:
+            return False
+        import torch
+        from .. import _lib
+        blocks = {k: torch.zeros((r1 - r0, self.N), dtype=torch.float32, device="cuda") for k in self.Ds}
+        for c0 in range(0, len(pairs), PAIR_CHUNK):
+            chunk = pairs[c0:c0 + PAIR_CHUNK]
+            sc = self._device_scores(chunk)
+            p = torch.as_tensor(np.asarray(chunk, np.int64)).cuda()
+            for k in blocks:
+                blocks[k][p[:, 0] - r0, p[:, 1]] = sc[k]
+        for k, blk in blocks.items():
+            full = _dist.all_gather_stripes(blk, bounds) if world > 1 else blk
+            if symmetric:
+                _lib.ds_finish(full, symmetric=True)
+            self.Ds[k][:] = full.cpu().numpy()
+        return True
 
     def _gather_stripes(self, bounds, r0, r1):
         import torch
@@ -141,17 +188,42 @@ class CoverAlgorithm(object):
             full = _dist.all_gather_stripes(blk, bounds)
             self.Ds[key][:] = full.cpu().numpy()
 
+    def _finish_device(self, norm, mode):
+        """normalize_by_length on the device for every Ds key (acoss_ds_finish, mode 'serra09' or
+        'chen'): one upload, one HIP kernel, one download per matrix."""
+        import torch
+        from .. import _lib
+        norm = np.asarray(norm, np.float64)
+        for key in list(self.Ds):
+            D = torch.as_tensor(np.ascontiguousarray(self.Ds[key], np.float32)).cuda()
+            _lib.ds_finish(D, norm, symmetric=False, mode=mode)
+            self.Ds[key][:] = D.cpu().numpy()
+
     def _save_Ds(self, prefix):
-        np.savez("%s_Ds.npz" % prefix, **{k: np.asarray(v) for k, v in self.Ds.items()})
+        """'<prefix>_Ds.h5' (h5py, one float32 dataset per similarity type) when h5py is
+        importable, and always the '<prefix>_Ds.npz' twin."""
+        mats = {k: np.asarray(v) for k, v in self.Ds.items()}
+        np.savez("%s_Ds.npz" % prefix, **mats)
+        try:
+            import h5py
+        except ImportError:
+            return
+        from ..features_io import save_h5
+        save_h5("%s_Ds.h5" % prefix, mats, h5py)
 
     def _load_Ds(self, prefix):
+        """The reference reads '<prefix>_Ds.h5' (:164-166); here the .h5 when h5py is importable,
+        else the .npz twin."""
         npz, h5 = "%s_Ds.npz" % prefix, "%s_Ds.h5" % prefix
-        if os.path.exists(npz):
-            with np.load(npz, allow_pickle=False) as z:
-                self.Ds = {k: np.array(z[k]) for k in z.files}
-        else:
-            from ..features_io import _load_h5
-            self.Ds = _load_h5(h5)
+        if os.path.exists(h5):
+            try:
+                from ..features_io import _load_h5
+                self.Ds = {k: np.asarray(v, np.float32) for k, v in _load_h5(h5).items()}
+                return
+            except ImportError:
+                pass
+        with np.load(npz, allow_pickle=False) as z:
+            self.Ds = {k: np.array(z[k]) for k in z.files}
 
     def cleanup_memmap(self):
         """Delete the memmap files of Ds (:195-203)."""
@@ -169,7 +241,11 @@ class CoverAlgorithm(object):
         a row to 'results_<shortname>_<name>.csv'."""
         D = np.array(self.Ds[similarity_type], dtype=np.float32)
         cliques = [sorted(self.cliques[s]) for s in self.cliques]
-        stats = evaluation.eval_statistics_cliques(D, cliques, topsidx)
+        if _on_gpu():  # the O(N^2) rank step as a HIP kernel (same statistics, same host code)
+            import torch
+            stats = evaluation.eval_statistics_device(torch.as_tensor(D).cuda(), cliques=cliques, topsidx=topsidx)
+        else:  # the reference's own host computation, restated (no GPU in this process)
+            stats = evaluation.eval_statistics_cliques(D, cliques, topsidx)
         MR, MRR, MDR, MAP, tops = stats
         if np.isnan(MR):
             warnings.warn("no clique with at least two songs")

@@ -33,12 +33,13 @@ class ChenFusion(ChromaBackedAlgorithm):
         self.Ds["qmax"][idxs[:, 0], idxs[:, 1]] = r["qmax"]
         self.Ds["dmax"][idxs[:, 0], idxs[:, 1]] = r["dmax"]
 
+    def _device_scores(self, idxs):
+        return self._score_dev(idxs, dmax=True)
+
     def normalize_by_length(self):
         """D[i, j] = sqrt(n_j) / D[i, j] (latefusion_chen.py:75-85): float64 quotient stored in
-        float32; a zero score gives inf, as in the reference (numpy warns)."""
-        norm = np.sqrt(np.array([self.load_features(j).shape[0] for j in range(self.N)], np.float64))
-        for key in self.Ds:
-            self.Ds[key][:] = norm[None, :] / np.asarray(self.Ds[key])
+        float32; a zero score gives inf, as in the reference (acoss_ds_finish mode 'chen')."""
+        self._finish_device(self._norm_factors(), "chen")
 
     def do_late_fusion(self):
         """SNF of all Ds (K=20, 20 iterations), then back to larger-is-closer (:87-91)."""

@@ -63,11 +63,17 @@ class ChromaBackedAlgorithm(CoverAlgorithm):
         self.prepare()
         return np.maximum(self._bank.lens.astype(np.int64) - self.m * self.tau, 1)
 
-    def _score(self, idxs, dmax=False):
+    def _score_dev(self, idxs, dmax=False):
         self.prepare()
-        res = self._bank.crp_align(np.asarray(idxs, np.int32), m=self.m, tau=self.tau, kappa=self.kappa,
-                                   oti=self.oti, qmax=True, dmax=dmax)
-        return {k: v.cpu().numpy() for k, v in res.items()}
+        return self._bank.crp_align(np.asarray(idxs, np.int32), m=self.m, tau=self.tau, kappa=self.kappa,
+                                    oti=self.oti, qmax=True, dmax=dmax)
+
+    def _score(self, idxs, dmax=False):
+        return {k: v.cpu().numpy() for k, v in self._score_dev(idxs, dmax).items()}
+
+    def _norm_factors(self):
+        """sqrt(n_j) in float64, n_j = downsampled frames of song j."""
+        return np.sqrt(np.array([self.load_features(j).shape[0] for j in range(self.N)], np.float64))
 
 
 class Serra09(ChromaBackedAlgorithm):
@@ -86,12 +92,15 @@ class Serra09(ChromaBackedAlgorithm):
         for key in self.Ds.keys():
             self.Ds[key][idxs[:, 0], idxs[:, 1]] = q
 
+    def _device_scores(self, idxs):
+        q = self._score_dev(idxs)["qmax"]
+        return {key: q for key in self.Ds}
+
     def normalize_by_length(self):
         """D[i, j] /= sqrt(n_j), n_j = downsampled frames of song j (rqa_serra09.py:71-83);
-        the quotient is taken in float64 and stored in the float32 matrix, as the reference."""
-        norm = np.sqrt(np.array([self.load_features(j).shape[0] for j in range(self.N)], np.float64))
-        for key in self.Ds.keys():
-            self.Ds[key][:] = np.asarray(self.Ds[key]) / norm[None, :]
+        the quotient is taken in float64 and stored in the float32 matrix, as the reference
+        (acoss_ds_finish mode 'serra09')."""
+        self._finish_device(self._norm_factors(), "serra09")
 
 
 def parser_args(args):

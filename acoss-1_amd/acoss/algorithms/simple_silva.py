@@ -79,6 +79,14 @@ class Simple(CoverAlgorithm):
         score, _ = _lib.simple_mp_packed(out, off, T, idxs.astype(np.int32), self.SSLEN)
         self.Ds['main'][idxs[:, 0], idxs[:, 1]] = -score.cpu().numpy()
 
+    def _device_scores(self, idxs):
+        """-median(MP) per ordered pair as float32 device scores (the memmap's dtype)."""
+        idxs = np.asarray(idxs)
+        self.prepare()
+        out, off, T = self._packed
+        score, _ = _lib.simple_mp_packed(out, off, T, idxs.astype(np.int32), self.SSLEN)
+        return {'main': (-score).float()}
+
 
 if __name__ == '__main__':
     parser = argparse.ArgumentParser(description="Benchmarking with Similarity Matrix Profile-based similarity",

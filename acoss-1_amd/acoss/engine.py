@@ -48,7 +48,9 @@ class ChromaBank:
         if pairs.numel() == 0:
             z = torch.zeros(0, dtype=torch.float32, device="cuda")
             return {k: z for k, on in (("qmax", qmax), ("dmax", dmax), ("oti", want_oti)) if on}
-        short = [i for i in np.unique(pairs.cpu().numpy()) if stacked_len(self.lens[i], m, tau) <= 0]
+        short = []
+        if stacked_len(int(self.lens.min()), m, tau) <= 0:  # only then can a pair hold a short track
+            short = [i for i in np.unique(pairs.cpu().numpy()) if stacked_len(self.lens[i], m, tau) <= 0]
         if short:
             raise ValueError("tracks %s are too short for frameStackSize=%d, frameStackStride=%d (essentia raises)"
                              % (short[:5], m, tau))

@@ -40,35 +40,27 @@ def eval_statistics(D, labels, topsidx=(1, 10, 100, 1000)):
     return eval_statistics_cliques(D, cliques, topsidx, presorted=True)
 
 
-def eval_statistics_cliques(D, cliques, topsidx=(1, 10, 100, 1000), presorted=False):
-    """getEvalStatistics on explicit cliques (lists of song indices, in the order of the
-    reference's `self.cliques` dict). Cliques are stably sorted by decreasing size (:219-225)
-    unless `presorted`."""
-    D = np.array(D, dtype=np.float32)
-    N = D.shape[0]
+def _ordered_cliques(cliques, presorted):
     Ks = np.array([len(c) for c in cliques], dtype=np.int64)
     if not presorted:
         order = np.argsort(-Ks, kind="stable")
         cliques = [cliques[i] for i in order]
         Ks = Ks[order]
     perm = np.array([i for c in cliques for i in c], dtype=np.int64)
-    D = D[perm][:, perm]
-    np.fill_diagonal(D, -np.inf)
+    return perm, Ks
+
+
+def _stats_from_ranks(member_ranks, Ks, N, topsidx):
+    """member_ranks(start, K, i) -> the 1-based ranks of the other members of the clique at
+    permuted positions [start, start + K) in the row of member i (permuted position)."""
     ranks = np.full(N, np.nan)
     allmap = np.full(N, np.nan)
-    # row-wise descending order, stable (index order breaks ties)
-    order = np.argsort(-D, axis=1, kind="stable")
-    pos = np.empty_like(order)
-    rows = np.arange(N)[:, None]
-    pos[rows, order] = np.arange(N)[None, :]
     start = 0
     for K in Ks:
         if K < 2:
             break
-        members = np.arange(start, start + K)
-        for i in members:
-            others = members[members != i]
-            r = np.sort(pos[i, others]) + 1
+        for i in range(start, start + K):
+            r = np.sort(member_ranks(start, K, i))
             ranks[i] = r[0]
             allmap[i] = np.mean(np.arange(1, K) / r)
         start += K
@@ -79,6 +71,66 @@ def eval_statistics_cliques(D, cliques, topsidx=(1, 10, 100, 1000), presorted=Fa
     MDR = np.median(ranks) if len(ranks) else np.nan
     tops = np.array([np.sum(ranks <= t) for t in topsidx], dtype=np.float64)
     return MR, MRR, MDR, MAP, tops
+
+
+def eval_statistics_cliques(D, cliques, topsidx=(1, 10, 100, 1000), presorted=False):
+    """getEvalStatistics on explicit cliques (lists of song indices, in the order of the
+    reference's `self.cliques` dict). Cliques are stably sorted by decreasing size (:219-225)
+    unless `presorted`."""
+    D = np.array(D, dtype=np.float32)
+    N = D.shape[0]
+    perm, Ks = _ordered_cliques(cliques, presorted)
+    D = D[perm][:, perm]
+    np.fill_diagonal(D, -np.inf)
+    # row-wise descending order, stable (index order breaks ties)
+    order = np.argsort(-D, axis=1, kind="stable")
+    pos = np.empty_like(order)
+    rows = np.arange(N)[:, None]
+    pos[rows, order] = np.arange(N)[None, :]
+
+    def member_ranks(start, K, i):
+        members = np.arange(start, start + K)
+        return pos[i, members[members != i]] + 1
+    return _stats_from_ranks(member_ranks, Ks, N, topsidx)
+
+
+def eval_statistics_device(D, labels=None, cliques=None, topsidx=(1, 10, 100, 1000)):
+    """eval_statistics / eval_statistics_cliques on a device-resident (N, N) float32 torch
+    matrix: the O(N^2) rank step runs as one HIP kernel (acoss_eval_ranks: the clique members'
+    positions in each query row's stable descending order, no sort materialised); the O(N)
+    statistics are the same host code as above, so the result is identical to the host path."""
+    from . import _lib
+    if cliques is None:
+        perm, Ks = clique_order(labels)
+        perm = perm.astype(np.int64)
+        Ks = np.asarray(Ks, np.int64)
+    else:
+        perm, Ks = _ordered_cliques(cliques, False)
+    N = int(D.shape[0])
+    pos = np.empty(N, np.int32)
+    pos[perm] = np.arange(N, dtype=np.int32)
+    q_song, m_off, members, where = [], [0], [], {}
+    start = 0
+    for K in Ks:
+        if K < 2:
+            break
+        for i in range(start, start + K):
+            where[i] = len(q_song)
+            q_song.append(perm[i])
+            others = [perm[t] for t in range(start, start + K) if t != i]
+            members.extend(others)
+            m_off.append(len(members))
+        start += K
+    if q_song:
+        r = _lib.eval_ranks(D, pos, np.asarray(q_song, np.int32), np.asarray(m_off, np.int64),
+                            np.asarray(members, np.int32)).astype(np.int64)
+    else:
+        r = np.zeros(0, np.int64)
+
+    def member_ranks(start, K, i):
+        q = where[i]
+        return r[m_off[q]:m_off[q + 1]]
+    return _stats_from_ranks(member_ranks, Ks, N, topsidx)
 
 
 def write_results_csv(resultsfile, name, similarity_type, stats, topsidx=(1, 10, 100, 1000)):

@@ -65,6 +65,15 @@ def _load_h5(path):
         return walk(f)
 
 
+def save_h5(path, mats, h5py):
+    """A dict of arrays as an HDF5 file in deepdish's dict layout (one dataset per key under
+    the root group), for the reference's '<prefix>_Ds.h5' (algorithm_template.py:193)."""
+    with h5py.File(path, "w") as f:
+        f.attrs["DEEPDISH_IO_VERSION"] = 12
+        for k, v in mats.items():
+            f.create_dataset(str(k), data=np.asarray(v))
+
+
 def load_features(path):
     """Feature dict of one track; IOError if no readable file exists."""
     if os.path.exists(path) and not path.endswith(".npz"):

@@ -92,6 +92,83 @@ def make_corpus(shape="covers80", frames=2000, frames_jitter=0.0, seed=SEED, str
     return tracks, np.asarray(labels, np.int32)
 
 
+# A corpus on which the score ranks are not saturated (MAP well below 1), so a MAP/MR1
+# comparison between two score matrices can detect a difference (SURVEY §8d "MAP parity").
+# Unrelated songs share chord phrases from one global pool (a progression of 4-8 triads with
+# its own dwells), and covers are partial, locally re-harmonised, noisier excerpts.
+HARD = {"pool": 24, "phrases": (3, 8), "noise": 0.3, "stretch": (0.7, 1.4), "excerpt": (0.5, 1.0),
+        "substitute": 0.25}
+
+
+def _phrase_pool(rng, n_phrases):
+    pool = []
+    for _ in range(n_phrases):
+        k = int(rng.integers(4, 9))
+        pool.append((rng.integers(0, 24, size=k), rng.integers(8, 41, size=k)))
+    return pool
+
+
+def _hard_base(rng, n, pool, per_song):
+    """A song = a few phrases of the shared pool (its own pick and order, transposed by one
+    random key per phrase), repeated until n frames."""
+    T = triad_templates()
+    picks = rng.choice(len(pool), size=per_song, replace=False)
+    keys = rng.integers(0, 12, size=per_song)
+    out = np.empty((n, 12), np.float32)
+    i, p = 0, 0
+    while i < n:
+        chords, dwells = pool[picks[p % per_song]]
+        key = int(keys[p % per_song])
+        for c, d in zip(chords, dwells):
+            if i >= n:
+                break
+            c = int(c)
+            root, minor = (c % 12 + key) % 12, c // 12
+            out[i:i + int(d)] = T[root + 12 * minor]
+            i += int(d)
+        p += 1
+    return out
+
+
+def _hard_cover(rng, base, n_out, params):
+    T = triad_templates()
+    lo, hi = params["excerpt"]
+    frac = float(rng.uniform(lo, hi))
+    seg = max(16, int(round(len(base) * frac)))
+    st = int(rng.integers(0, len(base) - seg + 1))
+    part = base[st:st + seg].copy()
+    # re-harmonise: each chord run is replaced by a random triad with probability `substitute`
+    edges = np.flatnonzero(np.any(part[1:] != part[:-1], axis=1)) + 1
+    bounds = np.concatenate([[0], edges, [len(part)]])
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        if rng.random() < params["substitute"]:
+            part[a:b] = T[int(rng.integers(0, 24))]
+    if n_out is None:
+        n_out = max(16, int(round(len(base) * float(rng.uniform(*params["stretch"])))))
+    idx = np.minimum((np.arange(n_out) * (len(part) / n_out)).astype(np.int64), len(part) - 1)
+    return np.roll(part[idx], int(rng.integers(0, 12)), axis=1)
+
+
+def make_hard_corpus(shape="covers80", frames=2000, seed=SEED, fixed_length=True, params=None):
+    """(tracks, labels) of the discriminative corpus (HARD). fixed_length: every track has
+    exactly `frames` frames (the bench's metric config, M = N = frames); else covers are
+    stretched by params['stretch']."""
+    params = dict(HARD, **(params or {}))
+    rng = np.random.Generator(np.random.PCG64(seed))
+    pool = _phrase_pool(rng, params["pool"])
+    tracks, labels = [], []
+    for lab, size in enumerate(clique_sizes(shape)):
+        base = _hard_base(rng, frames, pool, int(rng.integers(params["phrases"][0], params["phrases"][1] + 1)))
+        for v in range(size):
+            seq = base if v == 0 else _hard_cover(rng, base, frames if fixed_length else None, params)
+            x = seq + np.abs(rng.normal(0.0, params["noise"], seq.shape)).astype(np.float32)
+            x = _unitmax(x)
+            x[rng.random(len(x)) < 0.02] = 0.0
+            tracks.append(x)
+            labels.append(lab)
+    return tracks, np.asarray(labels, np.int32)
+
+
 def pack(tracks):
     """List of (n_i, 12) -> (feats (sum n, 12) f32, off int64, len int32)."""
     lens = np.array([len(t) for t in tracks], np.int32)

@@ -1103,7 +1103,9 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   }
   // split sub-batches alternate between the caller's stream and a side stream, each with its
   // own key-plane buffer, so one sub-batch's selects overlap the next one's sweep
-  static const int nbuf = [] {
+  // read per call: bench.py takes its per-kernel profile with ACOSS_SPLIT_STREAMS=1, so the
+  // kernel durations of that call add up to its wall time
+  const int nbuf = [] {
     const char* e = getenv("ACOSS_SPLIT_STREAMS");
     const int v = e ? atoi(e) : 2;
     return v < 1 ? 1 : (v > 3 ? 3 : v);

@@ -6,7 +6,9 @@ Workload (configs[1]): covers80-shaped corpus (164 tracks: 77x2, 2x3, 1x4 clique
 12-d HPCP, every track exactly 2000 frames at the CSM input (M = N = 2000, M' = N' = 1991),
 essentia defaults m=9, tau=1, kappa=0.095, OTI on, gamma 0.5/0.5. A step = every unordered
 pair (i < j) of the corpus scored once = 13,366 pairs at N=1. Features are resident in HBM
-before the timed region.
+before the timed region. The default corpus is the discriminative one (synthetic.make_hard_corpus:
+shared chord phrases, partial re-harmonised covers; MAP about 0.8 at 2000 frames), so the MAP/MR1
+comparison against the oracle can fail; --corpus bench is the round-1/2 corpus (MAP 1.0).
 
 Multi-GPU (one process per GPU, torchrun): weak scaling. The corpus grows to
 round(164 * sqrt(N)) tracks (the covers80 clique pattern repeated), so each rank scores a
@@ -44,8 +46,48 @@ def ops_pair(M, N, m=9, tau=1):
     return 2.0 * 12 * M * N + 32.0 * Mp * Np
 
 
-def corpus_tracks(n_gpus, frames, seed):
+# SURVEY.md §8d's 32 ops per CRP cell split by the kernel that does them: the sweep (Gram 2*12
+# per frame pair, 8 window adds, 2 norm terms, 1 sqrt), the two line selects and the mask (2
+# compares, 1 AND, 4 select), the DP (14).
+def ops_split(M, N, m=9, tau=1):
+    Mp = max(0, -(-(M - m * tau) // tau))
+    Np = max(0, -(-(N - m * tau) // tau))
+    cells = float(Mp * Np)
+    return {"sweep": 2.0 * 12 * M * N + 11.0 * cells, "selects": 7.0 * cells, "dp": 14.0 * cells}
+
+
+# library phase -> its share of ops_split (the fused row select runs inside the sweep kernel, so
+# the "sweep" phase carries the sweep's ops and half of the selects' ops; "select_cols" the rest)
+PHASE_OPS = {"sweep": lambda s: s["sweep"] + 0.5 * s["selects"], "select_cols": lambda s: 0.5 * s["selects"],
+             "dp_qmax": lambda s: s["dp"]}
+
+
+def log(msg):
+    """Progress on stderr (the JSON line is the only stdout output)."""
+    print("[bench %.1fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
+T_START = time.perf_counter()
+
+
+def host_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def corpus_tracks(n_gpus, frames, seed, kind="hard"):
     from acoss import synthetic
+    if kind == "hard" and n_gpus == 1:
+        return synthetic.make_hard_corpus("covers80", frames=frames, seed=seed)
     sizes = synthetic.clique_sizes("covers80")
     target = int(round(164 * math.sqrt(n_gpus)))
     pattern = []
@@ -59,6 +101,15 @@ def corpus_tracks(n_gpus, frames, seed):
         s = min(s, target - tot)
         out.append(s)
         tot += s
+    if kind == "hard":  # the covers80 pattern repeated to the weak-scaling corpus size
+        tracks, labels = [], []
+        rep = 0
+        while len(tracks) < target:
+            tr, lab = synthetic.make_hard_corpus("covers80", frames=frames, seed=seed + rep)
+            tracks += tr
+            labels += [int(v) + 80 * rep for v in lab]
+            rep += 1
+        return tracks[:target], np.asarray(labels[:target], np.int32)
     rng = np.random.Generator(np.random.PCG64(seed))
     tracks, labels = [], []
     for lab, size in enumerate(out):
@@ -77,8 +128,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--frames", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=20250101)
-    ap.add_argument("--cpu-sample", type=int, default=640, help="pairs timed on the CPU baseline (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--corpus", choices=["hard", "bench"], default="hard")
+    ap.add_argument("--cpu-sample", type=int, default=-1,
+                    help="pairs timed on the CPU baseline: -1 = the whole step (every pair, at N=1: it also gives "
+                         "the oracle-side MAP/MR1), 0 = skip, k = k random pairs")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
 
@@ -102,7 +156,8 @@ def main():
             dist.init_process_group(backend)
     n_gpus = world
 
-    tracks, labels = corpus_tracks(n_gpus, args.frames, args.seed)
+    tracks, labels = corpus_tracks(n_gpus, args.frames, args.seed, args.corpus)
+    log("corpus: %d tracks x %d frames (%s)" % (len(tracks), args.frames, args.corpus))
     T = len(tracks)
     lens = np.array([len(t) for t in tracks], np.int32)
     bank = ChromaBank(tracks)
@@ -123,6 +178,7 @@ def main():
         if world > 1:
             dist.barrier()
 
+    log("warmup")
     for _ in range(args.warmup):
         D = step()
     torch.cuda.synchronize()
@@ -142,21 +198,33 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = total_pairs * args.steps / dt
 
-    # ---- per-kernel HIP-event times of one profiled step (same stream, same launches) ----
+    # ---- one call of the path timed with HIP events on the stream it is launched on ----
+    # (a) as the timed steps run it (two streams: one sub-batch's selects overlap the next one's
+    #     sweep) -> roofline.achieved; (b) with ACOSS_SPLIT_STREAMS=1 and the library's per-phase
+    #     events, so the kernel durations add up to that call's time -> roofline.kernels
     phases = {}
-    call_ms = None
+    call_ms = call1_ms = None
     if not args.no_profile:
-        # one call of the path, HIP events on the stream it is launched on (the library's side
-        # stream joins back into it before the DP); per-kernel phases from the library's events
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        _lib.profile_enable(True)
         ev0.record()
         bank.crp_align(my_pairs, qmax=True)
         ev1.record()
         torch.cuda.synchronize()
         call_ms = ev0.elapsed_time(ev1)
+        prev = os.environ.get("ACOSS_SPLIT_STREAMS")
+        os.environ["ACOSS_SPLIT_STREAMS"] = "1"
+        _lib.profile_enable(True)
+        ev0.record()
+        bank.crp_align(my_pairs, qmax=True)
+        ev1.record()
+        torch.cuda.synchronize()
+        call1_ms = ev0.elapsed_time(ev1)
         phases = _lib.profile_read()
         _lib.profile_enable(False)
+        if prev is None:
+            del os.environ["ACOSS_SPLIT_STREAMS"]
+        else:
+            os.environ["ACOSS_SPLIT_STREAMS"] = prev
 
     # ---- MAP / MR1 on the assembled matrix (reference normalisation + evaluation) ----
     Dfull = D.cpu().numpy()                                       # (T, T) upper triangle filled
@@ -168,58 +236,94 @@ def main():
     if rank == 0:
         M = N = args.frames
         opp = ops_pair(M, N)
+        split = ops_split(M, N)
         launch_ms = call_ms if call_ms else ms_per_step
         batch_pairs = len(my_pairs_np)
-        kernels = {k: {"ms_per_launch": v[0] / max(1, v[1]), "launches": v[1]} for k, v in phases.items()}
-        dom = max(kernels.items(), key=lambda kv: kv[1]["ms_per_launch"] * kv[1]["launches"])[0] if kernels else None
+        kernels = {}
+        for k, v in phases.items():
+            ops = PHASE_OPS[k](split) * batch_pairs if k in PHASE_OPS else 0.0
+            kernels[k] = {"ms": round(v[0], 3), "launches": v[1],
+                          "tops": round(ops / (v[0] * 1e-3) / 1e12, 3) if ops and v[0] > 0 else None,
+                          "frac": round(ops / (v[0] * 1e-3) / 1e12 / PEAK_F32_TFLOPS, 4) if ops and v[0] > 0 else None}
+        dom = max(kernels.items(), key=lambda kv: kv[1]["ms"])[0] if kernels else None
         achieved = opp * batch_pairs / (launch_ms * 1e-3) / 1e12
-        traffic = None
-        tfile = os.path.join(ROOT, "profiles", "traffic_latest.json")
-        if os.path.exists(tfile):
-            try:  # measured on the default workload (profiles/profile.sh): only valid at that length
+        traffic, valu = None, None
+        for name, key in (("traffic_latest.json", "hbm_bytes_per_launch"), ("valu_latest.json", None)):
+            tfile = os.path.join(ROOT, "profiles", name)
+            if not os.path.exists(tfile):
+                continue
+            try:  # measured by profiles/profile.sh on the same workload: only valid at that length/corpus
                 tj = json.load(open(tfile))
-                traffic = tj.get("hbm_bytes_per_launch") if tj.get("frames") == args.frames else None
+                if tj.get("frames") != args.frames or tj.get("corpus", "bench") != args.corpus:
+                    continue
+                if key:
+                    traffic = tj.get(key)
+                else:
+                    valu = tj
             except Exception:
-                traffic = None
+                pass
         kernel_ms_sum = sum(v[0] for v in phases.values()) if phases else None
-        roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+        roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": traffic,
-                    "kernel": "acoss_crp_align (one call = oti + sweep + select_rows + select_cols + dp_qmax on "
+                    "kernel": "acoss_crp_align (one call = oti + sweep/select_rows + select_cols + dp_qmax on "
                               "%d pairs; sub-batches on two streams)" % batch_pairs,
-                    "ops_per_pair": opp, "launch_ms": round(launch_ms, 3),
-                    "kernel_ms_sum": round(kernel_ms_sum, 3) if kernel_ms_sum else None,
-                    "dominant_kernel": dom, "kernels": kernels}
+                    "ops_per_pair": opp, "ops_split_per_pair": split, "launch_ms": round(launch_ms, 3),
+                    "one_stream_call_ms": round(call1_ms, 3) if call1_ms else None,
+                    "kernel_ms_sum_one_stream": round(kernel_ms_sum, 3) if kernel_ms_sum else None,
+                    "dominant_kernel": dom, "kernels": kernels,
+                    "valu_issue": valu}
 
-        cpu = None
-        if args.cpu_sample > 0:
+        map_parity, cpu = None, None
+        if args.cpu_sample != 0:
             import oracle
-            rng = np.random.Generator(np.random.PCG64(1234))
-            sel = rng.choice(len(my_pairs_np), size=min(args.cpu_sample, len(my_pairs_np)), replace=False)
-            sp = my_pairs_np[sel]
             from acoss.synthetic import pack
             feats, off, ln = pack(tracks)
-            nth = args.cpu_threads or min(16, os.cpu_count() or 1)
+            nth = args.cpu_threads or len(os.sched_getaffinity(0))
+            if args.cpu_sample < 0 and world == 1:
+                sp = my_pairs_np
+                what = "the whole step: all %d pairs of the corpus" % len(sp)
+            else:
+                rng = np.random.Generator(np.random.PCG64(1234))
+                k = len(my_pairs_np) if args.cpu_sample < 0 else min(args.cpu_sample, len(my_pairs_np))
+                k = min(k, 640) if world > 1 else k
+                sp = my_pairs_np[rng.choice(len(my_pairs_np), size=k, replace=False)]
+                what = "%d random pairs of the same corpus" % len(sp)
+            log("cpu baseline: %s on %d threads" % (what, nth))
             t0 = time.perf_counter()
             q, _, _ = oracle.crp_batch(feats, off, ln, sp, dmax=False, nthreads=nth)
             cdt = time.perf_counter() - t0
             gq = Dfull[sp[:, 0], sp[:, 1]]
-            parity = bool(np.array_equal(gq.astype(np.float32), q))
             cpu = {"value": round(len(sp) / cdt, 3), "unit": "song-pairs/s", "cores": nth, "kind": "port",
-                   "sample": "%d random pairs of the same corpus (%dx%d frames), oracle/crp_oracle.cpp, "
-                             "%d OpenMP threads, %.1f s" % (len(sp), args.frames, args.frames, nth, cdt),
-                   "qmax_bitexact_vs_gpu": parity}
+                   "sample": "%s (%dx%d frames), oracle/crp_oracle.cpp, %d OpenMP threads, %.1f s"
+                             % (what, args.frames, args.frames, nth, cdt),
+                   "host": host_info(),
+                   "qmax_bitexact_vs_gpu": bool(np.array_equal(gq.astype(np.float32), q)),
+                   "qmax_pairs_differing": int(np.sum(gq.astype(np.float32) != q))}
+            if len(sp) == total_pairs:  # the oracle scored every pair: MAP/MR1 on its own matrix
+                Do = np.zeros_like(Dfull)
+                Do[sp[:, 0], sp[:, 1]] = q
+                Dos = (Do + Do.T).astype(np.float32)
+                Dos = (Dos / np.sqrt(lens.astype(np.float64))[None, :]).astype(np.float32)
+                oMR, oMRR, oMDR, oMAP, otops = evaluation.eval_statistics(Dos, labels)
+                map_parity = {"gpu": {"MAP": float(MAP), "MR1": float(MR), "MRR": float(MRR), "MDR": float(MDR),
+                                      "top": [int(t) for t in tops]},
+                              "oracle": {"MAP": float(oMAP), "MR1": float(oMR), "MRR": float(oMRR),
+                                         "MDR": float(oMDR), "top": [int(t) for t in otops]},
+                              "ds_bitexact": bool(np.array_equal(Dos, Dsym)),
+                              "identical": bool(np.array_equal(Dos, Dsym) and MAP == oMAP and MR == oMR)}
 
         result = {
             "metric": "song-pairs/sec (CSM+Qmax) on 12-d HPCP, ~2000 frames/track; MAP parity",
             "value": round(value, 2), "unit": "song-pairs/s", "n_gpus": n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "covers80-shaped synthetic HPCP, Serra09 CRP+Qmax, all unordered pairs",
+            "config": {"workload": "covers80-shaped synthetic HPCP (%s corpus), Serra09 CRP+Qmax, all unordered pairs"
+                                   % args.corpus,
                        "tracks": T, "pairs_per_step": total_pairs, "frames_per_track": args.frames,
                        "m": 9, "tau": 1, "kappa": 0.095, "oti": True, "parallelism": "pair-matrix row stripes dp%d"
                        % n_gpus},
             "map": round(float(MAP), 6), "mr1": round(float(MR), 4), "mrr": round(float(MRR), 6),
-            "top1": int(tops[0]),
+            "top1": int(tops[0]), "map_parity": map_parity,
             "roofline": roofline, "cpu_baseline": cpu,
             "speedup_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
         }

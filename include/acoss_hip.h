@@ -171,6 +171,25 @@ int acoss_earlyfusion(const float* mfcc, const float* ssm, const float* chroma, 
                       int32_t d_mfcc, int32_t d_ssm, int32_t d_chroma, const int32_t* pairs, int64_t n_pairs,
                       double kappa, int32_t K, float mu, double* scores_out, void* hip_stream);
 
+/* Finish of a pair-score matrix after the pair loop, in place when out == D.
+ * D, out: (n x n) float32, row stride ld (elements). symmetric = 1 first forms D[i,j] + D[j,i] from
+ * the original values (CoverAlgorithm.all_pairwise's `Ds += Ds.T`, algorithm_template.py:188-191);
+ * mode 0 stops there, 1 divides by norm[j] (Serra09.normalize_by_length, rqa_serra09.py:71-83),
+ * 2 stores norm[j] / D (ChenFusion.normalize_by_length, latefusion_chen.py:75-85); norm: float64[n]
+ * = sqrt(frames of song j), the quotient taken in float64 and rounded to float32 as the
+ * reference's float32 memmap does. */
+int acoss_ds_finish(const float* D, int32_t n, int64_t ld, const double* norm, int32_t symmetric, int32_t mode,
+                    float* out, void* hip_stream);
+
+/* The rank step of CoverAlgorithm.getEvalStatistics (algorithm_template.py:206-291): for query q
+ * (song q_song[q]) and each song j = members[m_off[q] .. m_off[q+1]), ranks_out[that index] = the
+ * 1-based position of j in np.argsort(-D', 1, kind="stable") of the query's row, where D' is D
+ * with the diagonal set to -inf (:234) and columns ordered by pos[] (each song's position in the
+ * reference's clique ordering, :220-230; NaN scores sort last). D: (n x n) float32, stride ld. */
+int acoss_eval_ranks(const float* D, int32_t n, int64_t ld, const int32_t* pos, const int32_t* q_song,
+                     const int64_t* m_off, const int32_t* members, int32_t n_queries, int32_t* ranks_out,
+                     void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,17 @@ def lib():
         L.or_oti.argtypes = [_fp, _fp]
         L.or_simple_oti.restype = ctypes.c_int
         L.or_simple_oti.argtypes = [_dp, ctypes.c_int, _dp, ctypes.c_int]
+        L.or_ess_compare_batch.restype = ctypes.c_int
+        L.or_ess_compare_batch.argtypes = [_fp, _i64p, _i32p, _i32p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_float, ctypes.c_float, _i64p, _fp, _fp, _i32p, _i32p,
+                                           ctypes.c_int]
+        L.or_ess_dist.restype = ctypes.c_int64
+        L.or_ess_dist.argtypes = [_fp, ctypes.c_int, _fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, _fp]
+        L.or_ess_profile.argtypes = [_fp, ctypes.c_int, ctypes.c_int, _fp]
+        L.or_ess_oti.restype = ctypes.c_int
+        L.or_ess_oti.argtypes = [_fp, _fp, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -117,6 +128,51 @@ def crp_batch(feats, off, lens, pairs, m=9, tau=1, kappa=0.095, oti=True, gamma_
     if rc != 0:
         raise ValueError("a track is too short for the stacking")
     return q, (d if dmax else None), k
+
+
+ESS_STATS = ("cells", "flips", "d_diff", "neg_items", "eq_thr", "thr_diff", "ones_canon", "ones_ess")
+ESS_ACC = {"f32": 0, "f64": 1, "f32fma": 2}
+
+
+def ess_compare(feats, off, lens, pairs, acc="f32", prof_mean=False, strict=False, pct_literal=False, m=9, tau=1,
+                kappa=0.095, gamma_open=0.5, gamma_ext=0.5, nthreads=0):
+    """Canonical (the HIP kernels' order) vs essentia-order (crp_oracle.cpp or_ess_*) CRP + Qmax
+    of every pair. Returns (stats (P, 8) int64 with columns ESS_STATS, qmax_canon, qmax_ess,
+    oti_canon, oti_ess)."""
+    feats = np.ascontiguousarray(feats, np.float32)
+    off = np.ascontiguousarray(off, np.int64)
+    lens = np.ascontiguousarray(lens, np.int32)
+    pairs = np.ascontiguousarray(pairs, np.int32)
+    P = len(pairs)
+    st = np.zeros((P, 8), np.int64)
+    qc, qe = np.zeros(P, np.float32), np.zeros(P, np.float32)
+    oc, oe = np.zeros(P, np.int32), np.zeros(P, np.int32)
+    rc = lib().or_ess_compare_batch(_p(feats, _fp), _p(off, _i64p), _p(lens, _i32p), _p(pairs, _i32p), P, m, tau,
+                                    kappa, ESS_ACC[acc], int(prof_mean), int(strict), int(pct_literal), gamma_open,
+                                    gamma_ext, _p(st, _i64p), _p(qc, _fp), _p(qe, _fp), _p(oc, _i32p), _p(oe, _i32p),
+                                    int(nthreads))
+    if rc != 0:
+        raise ValueError("a track is too short for the stacking")
+    return st, qc, qe, oc, oe
+
+
+def ess_dist(X, Y, k=0, m=9, tau=1, acc="f32"):
+    """essentia-order stacked pairwise distance (negative items -> NaN, as sqrt does)."""
+    X = np.ascontiguousarray(X, np.float32)
+    Y = np.ascontiguousarray(Y, np.float32)
+    Mp, Np = stacked_len(len(X), m, tau), stacked_len(len(Y), m, tau)
+    D = np.zeros((Mp, Np), np.float32)
+    neg = lib().or_ess_dist(_p(X, _fp), len(X), _p(Y, _fp), len(Y), int(k), m, tau, ESS_ACC[acc], _p(D, _fp))
+    return D, int(neg)
+
+
+def ess_oti(X, Y, acc="f32", prof_mean=False):
+    X = np.ascontiguousarray(X, np.float32)
+    Y = np.ascontiguousarray(Y, np.float32)
+    pq, pr = np.zeros(12, np.float32), np.zeros(12, np.float32)
+    lib().or_ess_profile(_p(X, _fp), len(X), int(prof_mean), _p(pq, _fp))
+    lib().or_ess_profile(_p(Y, _fp), len(Y), int(prof_mean), _p(pr, _fp))
+    return int(lib().or_ess_oti(_p(pq, _fp), _p(pr, _fp), ESS_ACC[acc]))
 
 
 def align(C, gamma_open=0.5, gamma_ext=0.5, which=0):

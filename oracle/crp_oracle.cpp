@@ -100,39 +100,47 @@ void or_stacked_norms(const float* nx, int n, int m, int tau, float* NX) {
 }
 
 // D (Mp x Np, row-major). Y is rotated by k (np.roll semantics on the chroma axis).
+// Loops run across j so the compiler vectorises them; every element keeps the canonical
+// sequential order (c for the Gram fma chain, t for the window sum).
 void or_crp_dist(const float* X, int M, const float* Y, int N, int k, int m, int tau, float* D) {
   const int Mp = or_stacked_len(M, m, tau), Np = or_stacked_len(N, m, tau);
   if (Mp <= 0 || Np <= 0) return;
-  std::vector<float> nx(M), ny(N), NX(Mp), NY(Np), Yr((size_t)N * 12);
-  for (int b = 0; b < N; ++b)
-    for (int c = 0; c < 12; ++c) Yr[(size_t)b * 12 + c] = Y[(size_t)b * 12 + ((c - k + 12) % 12)];
+  std::vector<float> nx(M), ny(N), NX(Mp), NY(Np);
   or_frame_norms(X, M, nx.data());
   or_frame_norms(Y, N, ny.data());
   or_stacked_norms(nx.data(), M, m, tau, NX.data());
   or_stacked_norms(ny.data(), N, m, tau, NY.data());
-  // G only at the (a, b) used: a, b multiples of tau. Compute per row pair on the fly.
-  const int Ma = (Mp - 1 + m) , Nb = (Np - 1 + m);  // stacked-frame grid extents
-  std::vector<float> G((size_t)Ma * Nb);
+  // G only at the (a, b) used: frames a*tau, b*tau of the stacked-frame grid.
+  const int Ma = (Mp - 1 + m), Nb = (Np - 1 + m);
+  std::vector<float> YT((size_t)12 * Nb), G((size_t)Ma * Nb), acc(Np);
+  for (int jb = 0; jb < Nb; ++jb)
+    for (int c = 0; c < 12; ++c) YT[(size_t)c * Nb + jb] = Y[(size_t)jb * tau * 12 + ((c - k + 12) % 12)];
   for (int ia = 0; ia < Ma; ++ia) {
     const float* x = X + (size_t)ia * tau * 12;
-    for (int jb = 0; jb < Nb; ++jb) {
-      const float* y = Yr.data() + (size_t)jb * tau * 12;
-      float acc = 0.0f;
-      for (int c = 0; c < 12; ++c) acc = fmaf(x[c], y[c], acc);
-      G[(size_t)ia * Nb + jb] = acc;
+    float* g = G.data() + (size_t)ia * Nb;
+    for (int jb = 0; jb < Nb; ++jb) g[jb] = 0.0f;
+    for (int c = 0; c < 12; ++c) {
+      const float xc = x[c];
+      const float* yc = YT.data() + (size_t)c * Nb;
+      for (int jb = 0; jb < Nb; ++jb) g[jb] = __builtin_fmaf(xc, yc[jb], g[jb]);
     }
   }
   for (int i = 0; i < Mp; ++i) {
+    for (int j = 0; j < Np; ++j) acc[j] = 0.0f;
+    for (int t = 0; t < m; ++t) {
+      const float* g = G.data() + (size_t)(i + t) * Nb + t;
+      for (int j = 0; j < Np; ++j) acc[j] = acc[j] + g[j];
+    }
+    float* d = D + (size_t)i * Np;
+    const float nxi = NX[i];
     for (int j = 0; j < Np; ++j) {
-      float dot = 0.0f;
-      for (int t = 0; t < m; ++t) dot = dot + G[(size_t)(i + t) * Nb + (j + t)];
-      const float d2 = (NX[i] - 2.0f * dot) + NY[j];
-      D[(size_t)i * Np + j] = d2 > 0.0f ? sqrtf(d2) : 0.0f;
+      const float d2 = (nxi - 2.0f * acc[j]) + NY[j];
+      d[j] = d2 > 0.0f ? sqrtf(d2) : 0.0f;
     }
   }
 }
 
-// essentia percentile (essentiamath.h), restated; sorts v in place.
+// essentia percentile (essentiamath.h), restated; s is the sorted line.
 float or_percentile_sorted(const float* s, int n, float kappa) {
   const float q = (float)(n - 1) * kappa;
   const float lo = floorf(q), hi = ceilf(q);
@@ -142,18 +150,37 @@ float or_percentile_sorted(const float* s, int n, float kappa) {
   return a + b;
 }
 
-void or_crp_thresholds(const float* D, int Mp, int Np, float kappa, float* thr_r, float* thr_c) {
+// The same value without sorting the whole line: only the order statistics at floor(q) and
+// ceil(q) enter the interpolation, so nth_element + the minimum above it give them exactly.
+// literal = 1: essentia's d0 + d1 form with no integer-q case (an integer q gives 0).
+static float pct_select(float* v, int n, float kappa, int literal) {
+  const float q = (float)(n - 1) * kappa;
+  const float lo = floorf(q), hi = ceilf(q);
+  const int ilo = (int)lo, ihi = (int)hi;
+  std::nth_element(v, v + ilo, v + n);
+  const float slo = v[ilo];
+  const float shi = (ihi == ilo) ? slo : *std::min_element(v + ilo + 1, v + n);
+  if (lo == hi && !literal) return slo;
+  const float a = slo * (hi - q);
+  const float b = shi * (q - lo);
+  return a + b;
+}
+
+static void crp_thresholds_impl(const float* D, int Mp, int Np, float kappa, int literal, float* thr_r,
+                                float* thr_c) {
   std::vector<float> v(std::max(Mp, Np));
   for (int i = 0; i < Mp; ++i) {
     std::copy(D + (size_t)i * Np, D + (size_t)(i + 1) * Np, v.begin());
-    std::sort(v.begin(), v.begin() + Np);
-    thr_r[i] = or_percentile_sorted(v.data(), Np, kappa);
+    thr_r[i] = pct_select(v.data(), Np, kappa, literal);
   }
   for (int j = 0; j < Np; ++j) {
     for (int i = 0; i < Mp; ++i) v[i] = D[(size_t)i * Np + j];
-    std::sort(v.begin(), v.begin() + Mp);
-    thr_c[j] = or_percentile_sorted(v.data(), Mp, kappa);
+    thr_c[j] = pct_select(v.data(), Mp, kappa, literal);
   }
+}
+
+void or_crp_thresholds(const float* D, int Mp, int Np, float kappa, float* thr_r, float* thr_c) {
+  crp_thresholds_impl(D, Mp, Np, kappa, 0, thr_r, thr_c);
 }
 
 void or_crp_mask(const float* D, int Mp, int Np, const float* thr_r, const float* thr_c, uint8_t* C) {
@@ -248,6 +275,219 @@ int or_crp_batch(const float* feats, const int64_t* off, const int32_t* len, con
     if (qmax) qmax[p] = qv;
     if (dmax) dmax[p] = dv;
     if (oti) oti[p] = k;
+  }
+  return err ? -1 : 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// essentia-order restatement (comparison mode; NOT what the HIP kernels reproduce).
+//
+// essentia ChromaCrossSimilarity::compute [ext, essentia 2.1-beta6-dev, unpinned] as its
+// published source reads, restated literally rather than in the canonical decomposed order:
+//   globalAverageChroma = sumFrames (sequential f32 adds per bin) [mean variant: / nframes],
+//                         then normalize() (each bin / max bin)
+//   optimalTranspositionIndex: for i = 0..noti(12): rotate the reference profile right by
+//                         one (std::rotate, i > 0), dotProduct(query, reference); argmax
+//                         (first maximum)
+//   rotateChroma(reference, oti): every frame rotated right by oti (np.roll)
+//   stackChromaFrames(m, tau): row s = frames s*tau .. s*tau + (m-1)*tau concatenated (m*12-d)
+//   pairwiseDistance: item = dotProduct(a,a) - 2*dotProduct(a,b) + dotProduct(b,b);
+//                     D = sqrt(item) (a negative item gives NaN: counted, see n_neg)
+//   dotProduct = std::inner_product over the m*12 products. The accumulator is the open
+//     question; `acc` selects it:
+//       0  float accumulator, product rounded to float, then a separate add (init (T)0.0,
+//          no contraction: a generic x86-64 build has no FMA)
+//       1  double accumulator (init 0.0): float product, widened, added in double, the sum
+//          rounded to float on return
+//       2  float accumulator with the multiply-add contracted into fmaf (an -march=native
+//          build with FMA and GCC's default -ffp-contract=fast)
+//   percentile(line, 9.5): sort, k = (n-1)*0.095f, d0 + d1 interpolation; pct_literal = 1
+//     drops the integer-k special case of the canonical restatement (d0 + d1 = 0 there)
+//   binarize: C = (D <= thr_row) * (D <= thr_col); strict = 1 uses < (the other Heaviside)
+// Nothing but tests/golden/make_essentia_bound.py and tests/ call this.
+// ------------------------------------------------------------------------------------------
+static inline float ess_dot(const float* a, const float* b, int n, int acc) {
+  if (acc == 1) {
+    double s = 0.0;
+    for (int e = 0; e < n; ++e) {
+      const float p = a[e] * b[e];
+      s = s + (double)p;
+    }
+    return (float)s;
+  }
+  float s = 0.0f;
+  if (acc == 2) {
+    for (int e = 0; e < n; ++e) s = __builtin_fmaf(a[e], b[e], s);
+  } else {
+    for (int e = 0; e < n; ++e) {
+      const float p = a[e] * b[e];
+      s = s + p;
+    }
+  }
+  return s;
+}
+
+void or_ess_profile(const float* X, int n, int mean, float* prof) {
+  float s[12];
+  for (int c = 0; c < 12; ++c) s[c] = 0.0f;
+  for (int c = 0; c < 12; ++c)
+    for (int t = 0; t < n; ++t) s[c] = s[c] + X[(size_t)t * 12 + c];
+  if (mean)
+    for (int c = 0; c < 12; ++c) s[c] = s[c] / (float)n;
+  float mx = s[0];
+  for (int c = 1; c < 12; ++c)
+    if (s[c] > mx) mx = s[c];
+  for (int c = 0; c < 12; ++c) prof[c] = mx != 0.0f ? s[c] / mx : s[c];
+}
+
+int or_ess_oti(const float* pq, const float* pr, int acc) {
+  float r[12];
+  for (int c = 0; c < 12; ++c) r[c] = pr[c];
+  int best = 0;
+  float bestv = 0.0f;
+  for (int i = 0; i <= 12; ++i) {
+    if (i > 0) {  // std::rotate(begin, end - 1, end): right by one
+      const float last = r[11];
+      for (int c = 11; c > 0; --c) r[c] = r[c - 1];
+      r[0] = last;
+    }
+    const float v = ess_dot(pq, r, 12, acc);
+    if (i == 0 || v > bestv) {
+      bestv = v;
+      best = i;
+    }
+  }
+  return best % 12;
+}
+
+// Literal pairwiseDistance over stacked vectors. Vectorised across j; each element keeps
+// the sequential inner_product order over e = t*12 + c. Returns the count of negative items.
+int64_t or_ess_dist(const float* X, int M, const float* Y, int N, int k, int m, int tau, int acc, float* D) {
+  const int Mp = or_stacked_len(M, m, tau), Np = or_stacked_len(N, m, tau);
+  if (Mp <= 0 || Np <= 0) return 0;
+  const int E = m * 12;
+  std::vector<float> XS((size_t)Mp * E), YST((size_t)E * Np), a(Mp), cc(Np), ys(E);
+  for (int s = 0; s < Mp; ++s)
+    for (int t = 0; t < m; ++t)
+      for (int c = 0; c < 12; ++c) XS[(size_t)s * E + t * 12 + c] = X[(size_t)(s * tau + t * tau) * 12 + c];
+  for (int s = 0; s < Np; ++s) {
+    for (int t = 0; t < m; ++t)
+      for (int c = 0; c < 12; ++c) ys[t * 12 + c] = Y[(size_t)(s * tau + t * tau) * 12 + ((c - k + 12) % 12)];
+    for (int e = 0; e < E; ++e) YST[(size_t)e * Np + s] = ys[e];
+    cc[s] = ess_dot(ys.data(), ys.data(), E, acc);
+  }
+  for (int s = 0; s < Mp; ++s) a[s] = ess_dot(&XS[(size_t)s * E], &XS[(size_t)s * E], E, acc);
+  int64_t neg = 0;
+  std::vector<float> bf(Np);
+  std::vector<double> bd(acc == 1 ? Np : 0);
+  for (int i = 0; i < Mp; ++i) {
+    const float* x = &XS[(size_t)i * E];
+    if (acc == 1) {
+      for (int j = 0; j < Np; ++j) bd[j] = 0.0;
+      for (int e = 0; e < E; ++e) {
+        const float xe = x[e];
+        const float* y = &YST[(size_t)e * Np];
+        for (int j = 0; j < Np; ++j) {
+          const float p = xe * y[j];
+          bd[j] = bd[j] + (double)p;
+        }
+      }
+      for (int j = 0; j < Np; ++j) bf[j] = (float)bd[j];
+    } else {
+      for (int j = 0; j < Np; ++j) bf[j] = 0.0f;
+      for (int e = 0; e < E; ++e) {
+        const float xe = x[e];
+        const float* y = &YST[(size_t)e * Np];
+        if (acc == 2) {
+          for (int j = 0; j < Np; ++j) bf[j] = __builtin_fmaf(xe, y[j], bf[j]);
+        } else {
+          for (int j = 0; j < Np; ++j) {
+            const float p = xe * y[j];
+            bf[j] = bf[j] + p;
+          }
+        }
+      }
+    }
+    float* d = D + (size_t)i * Np;
+    for (int j = 0; j < Np; ++j) {
+      const float item = (a[i] - 2.0f * bf[j]) + cc[j];
+      if (item < 0.0f) ++neg;
+      d[j] = sqrtf(item);
+    }
+  }
+  return neg;
+}
+
+// One pair in both modes. Per-pair outputs (index p):
+//   st[8*p + 0..7] = cells, mask bits that differ, cells whose D differs, negative items,
+//                    essentia cells equal to a threshold (where strict vs <= matters),
+//                    rows + columns whose threshold differs, CRP ones canonical, CRP ones essentia
+//   qc/qe = canonical / essentia Qmax; oc/oe = the two OTI indices.
+int or_ess_compare_batch(const float* feats, const int64_t* off, const int32_t* len, const int32_t* pairs,
+                         int64_t n_pairs, int m, int tau, float kappa, int acc, int prof_mean, int strict,
+                         int pct_literal, float g_open, float g_ext, int64_t* st, float* qc, float* qe,
+                         int32_t* oc, int32_t* oe, int nthreads) {
+  int err = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+#endif
+  for (int64_t p = 0; p < n_pairs; ++p) {
+    const int ia = pairs[2 * p], ib = pairs[2 * p + 1];
+    const float* X = feats + off[ia] * 12;
+    const float* Y = feats + off[ib] * 12;
+    const int M = len[ia], N = len[ib];
+    const int Mp = or_stacked_len(M, m, tau), Np = or_stacked_len(N, m, tau);
+    int64_t* s = st + 8 * p;
+    for (int u = 0; u < 8; ++u) s[u] = 0;
+    if (Mp <= 0 || Np <= 0) {
+      err |= 1;
+      continue;
+    }
+    float pq[12], pr[12];
+    or_track_profile(X, M, pq);
+    or_track_profile(Y, N, pr);
+    const int kc = or_oti(pq, pr);
+    or_ess_profile(X, M, prof_mean, pq);
+    or_ess_profile(Y, N, prof_mean, pr);
+    const int ke = or_ess_oti(pq, pr, acc);
+    oc[p] = kc;
+    oe[p] = ke;
+    const size_t cells = (size_t)Mp * Np;
+    std::vector<float> Dc(cells), De(cells), trc(Mp), tcc(Np), tre(Mp), tce(Np);
+    std::vector<uint8_t> Cc(cells), Ce(cells);
+    or_crp_dist(X, M, Y, N, kc, m, tau, Dc.data());
+    const int64_t neg = or_ess_dist(X, M, Y, N, ke, m, tau, acc, De.data());
+    crp_thresholds_impl(Dc.data(), Mp, Np, kappa, 0, trc.data(), tcc.data());
+    crp_thresholds_impl(De.data(), Mp, Np, kappa, pct_literal, tre.data(), tce.data());
+    or_crp_mask(Dc.data(), Mp, Np, trc.data(), tcc.data(), Cc.data());
+    int64_t flips = 0, ddiff = 0, eq = 0, onc = 0, one = 0;
+    for (int i = 0; i < Mp; ++i)
+      for (int j = 0; j < Np; ++j) {
+        const size_t t = (size_t)i * Np + j;
+        const float d = De[t];
+        const bool r = strict ? (d < tre[i]) : (d <= tre[i]);
+        const bool c = strict ? (d < tce[j]) : (d <= tce[j]);
+        Ce[t] = (uint8_t)(r && c);
+        eq += (d == tre[i]) || (d == tce[j]);
+        flips += Ce[t] != Cc[t];
+        ddiff += De[t] != Dc[t];
+        onc += Cc[t];
+        one += Ce[t];
+      }
+    int64_t thr_diff = 0;
+    for (int i = 0; i < Mp; ++i) thr_diff += trc[i] != tre[i];
+    for (int j = 0; j < Np; ++j) thr_diff += tcc[j] != tce[j];
+    s[0] = (int64_t)cells;
+    s[1] = flips;
+    s[2] = ddiff;
+    s[3] = neg;
+    s[4] = eq;
+    s[5] = thr_diff;
+    s[6] = onc;
+    s[7] = one;
+    qc[p] = or_align(Cc.data(), Mp, Np, g_open, g_ext, 0);
+    qe[p] = or_align(Ce.data(), Mp, Np, g_open, g_ext, 0);
   }
   return err ? -1 : 0;
 }

@@ -1,0 +1,47 @@
+"""One rank of tests/test_gpu_multirank.py (not a test module): runs a plugin's real HIP
+all_pairwise under torch.distributed (gloo; the ranks share one GPU) and rank 0 saves Ds.
+Usage: python tests/multirank_worker.py ALGO CSV FEATURE_DIR CACHEDIR OUT.npz
+(RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT from the environment)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (ROOT, os.path.join(ROOT, "acoss-1_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+
+def main():
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    algo, csv, fdir, cachedir, out = sys.argv[1:6]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    torch.cuda.set_device(0)
+    if world > 1:
+        dist.init_process_group("gloo")
+    os.makedirs(cachedir, exist_ok=True)
+    os.chdir(cachedir)
+    if algo == "Serra09":
+        from acoss.algorithms.rqa_serra09 import Serra09
+        a = Serra09(csv, fdir, shortname="mr", cachedir=cachedir)
+        a.all_pairwise(symmetric=True)
+        a.normalize_by_length()
+    elif algo == "ChenFusion":
+        from acoss.algorithms.latefusion_chen import ChenFusion
+        a = ChenFusion(csv, fdir, shortname="mr", cachedir=cachedir)
+        a.all_pairwise(symmetric=True)
+    else:
+        from acoss.algorithms.simple_silva import Simple
+        a = Simple(csv, fdir, shortname="mr", cachedir=cachedir)
+        a.all_pairwise(symmetric=False)
+    if rank == 0:
+        np.savez(out, **{k: np.asarray(v) for k, v in a.Ds.items()})
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

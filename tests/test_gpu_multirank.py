@@ -1,0 +1,78 @@
+"""The real HIP scorers under torch.distributed: 2 gloo ranks sharing one GPU each score a
+row stripe of a Da-TACOS-shaped mini corpus (13-song cliques plus singletons, ragged
+lengths) through Serra09 / ChenFusion / Simple.all_pairwise (algorithm_template.py:142-193),
+all-gather, symmetrise on the device; the assembled Ds must equal the world-1 run bit for bit.
+Ranks are child processes (subprocess), one GPU context each (3 with the parent)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from acoss import synthetic
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+WORKER = os.path.join(ROOT, "tests", "multirank_worker.py")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def datacos_mini(tmp_path_factory):
+    root = tmp_path_factory.mktemp("dtmini")
+    rng = np.random.Generator(np.random.PCG64(77))
+    tracks, labels = [], []
+    sizes = [13, 13, 13] + [1] * 9
+    for lab, size in enumerate(sizes):
+        base = synthetic.base_sequence(rng, int(rng.integers(200, 700)) * 40)
+        for v in range(size):
+            seq = base if v == 0 else synthetic.cover_of(rng, base)
+            tracks.append(synthetic.render(rng, seq))
+            labels.append(lab)
+    csv, fdir = synthetic.write_feature_dataset(str(root), tracks, np.asarray(labels))
+    return root, csv, fdir
+
+
+def _run(algo, world, root, csv, fdir, tag):
+    out = str(root / ("%s_%s_w%d.npz" % (algo, tag, world)))
+    cache = str(root / ("cache_%s_%s_w%d" % (algo, tag, world)))
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, WORKER, algo, csv, fdir, cache, out], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    logs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        logs.append(o.decode(errors="replace"))
+    for p, lg in zip(procs, logs):
+        assert p.returncode == 0, lg[-3000:]
+    with np.load(out) as z:
+        return {k: np.array(z[k]) for k in z.files}
+
+
+@pytest.mark.parametrize("algo", ["Serra09", "ChenFusion", "Simple"])
+def test_world2_equals_world1(datacos_mini, algo):
+    root, csv, fdir = datacos_mini
+    d1 = _run(algo, 1, root, csv, fdir, "a")
+    d2 = _run(algo, 2, root, csv, fdir, "b")
+    assert set(d1) == set(d2)
+    for k in d1:
+        assert d1[k].shape == (48, 48)
+        assert np.count_nonzero(d1[k]) > 48 * 30
+        np.testing.assert_array_equal(d2[k], d1[k])
