@@ -44,7 +44,7 @@ SIGNATURES = {
     "acoss_get_oti": [_vp, _vp, _i32, _vp, _vp],
     "acoss_binarize_rows": [_vp, _i32, _i32, _i32, _vp, _vp],
     "acoss_wcsm": [_vp, _i32, _i32, _i32, _i32, _f32, _vp, _vp],
-    "acoss_snf_step": [_vp, _i32, _i32, _i32, _vp, _vp, _i32, ctypes.c_double, _vp, _vp],
+    "acoss_snf_step": [_vp, _i32, _i32, _i32, _vp, _vp, _i32, ctypes.c_double, _vp, _i32, _vp],
     "acoss_simple_mp": [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _vp],
     "acoss_median_downsample": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
     "acoss_simple_features": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _i64, _vp],
@@ -123,6 +123,11 @@ def _check_pairs(pairs, n_tracks):
     """Host-side bounds check of (P, 2) track indices before a kernel dereferences them."""
     if pairs.numel() and (int(pairs.min()) < 0 or int(pairs.max()) >= n_tracks):
         raise ValueError("pair indices must lie in [0, %d)" % n_tracks)
+
+
+def check_knn(J, n):
+    """Public form of the kNN index check (see snf_step(validated=True))."""
+    _check_knn(J, n)
 
 
 def _check_knn(J, n):
@@ -312,11 +317,13 @@ def wcsm(CSM, k1, k2, mu=0.5):
     return out
 
 
-def snf_step(mats, skip, J, V, reg_diag, out=None):
+def snf_step(mats, skip, J, V, reg_diag, out=None, validated=False):
     """One doSimilarityFusionWs cross-diffusion step for matrix `skip`
     (similarity_fusion.py:163-174): S . mean_{m != skip}(mats[m]) . S^T + reg_diag * I.
     mats: list of (n, n) float64 device tensors; J (n, K) column indices, V (n, K) float64
-    row-normalised kNN weights of S. Returns a new (n, n) float64 device tensor (or `out`)."""
+    row-normalised kNN weights of S. Returns a new (n, n) float64 device tensor (or `out`).
+    validated=True: J (a device int32 tensor) was checked by `check_knn` already (the fusion loop
+    checks each S once, not once per step), so neither the host nor the library checks it again."""
     torch = _torch()
     lib = load_library()
     n = int(mats[0].shape[0])
@@ -329,12 +336,13 @@ def snf_step(mats, skip, J, V, reg_diag, out=None):
     Vd = _dev(V, torch.float64).contiguous()
     if Jd.shape != Vd.shape or Jd.dim() != 2 or Jd.shape[0] != n:
         raise ValueError("snf_step: J and V must both be (n, K)")
-    _check_knn(Jd, n)
+    if not validated:
+        _check_knn(Jd, n)
     if out is None:
         out = torch.empty((n, n), dtype=torch.float64, device=mats[0].device)
     ptrs = (ctypes.c_void_p * len(mats))(*[m.data_ptr() for m in mats])
     rc = lib.acoss_snf_step(ptrs, len(mats), int(skip), n, _ptr(Jd), _ptr(Vd), int(Jd.shape[1]), float(reg_diag),
-                            _ptr(out), _stream())
+                            _ptr(out), 0 if validated else 1, _stream())
     _check(rc, "acoss_snf_step")
     return out
 

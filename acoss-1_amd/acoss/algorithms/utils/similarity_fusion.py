@@ -144,13 +144,19 @@ def _fusion_ws(Ws, K=5, niters=20, reg_diag=1):
             warnings.warn("invalid value encountered in divide", RuntimeWarning, stacklevel=3)
             return torch.full(Pts[0].shape, float("nan"), dtype=torch.float64, device=Pts[0].device)
         return Pts[0].clone()
+    # each S is fixed across the iterations: its kNN columns are checked once here, and the
+    # steps skip the per-step check (and the stream sync it costs)
+    Js = [S.J.to(torch.int32).contiguous() for S in Ss]
+    Vs = [S.V.to(torch.float64).contiguous() for S in Ss]
+    for Jt in Js:
+        _lib.check_knn(Jt, Pts[0].shape[0])
     for it in range(niters):
         # the reference's `Pts = nextPts` aliasing: from the second iteration on, matrix i's
         # update already sees the new matrices k < i; replacing Pts[i] in place of the list
         # entry reproduces that, and the first iteration (separate lists) sees only old ones
         nxt = list(Pts) if it == 0 else Pts
         for i in range(N):
-            nxt[i] = _lib.snf_step(Pts, i, Ss[i].J, Ss[i].V, reg_diag)
+            nxt[i] = _lib.snf_step(Pts, i, Js[i], Vs[i], reg_diag, validated=True)
         Pts = nxt
     Fused = torch.zeros(Pts[0].shape, dtype=torch.float64, device=Pts[0].device)
     for Pt in Pts:

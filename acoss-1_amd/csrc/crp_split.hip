@@ -186,8 +186,16 @@ __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int str
   const int rows = PARTIAL ? min(kSR, V.Mp - i0) : kSR;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifdef ACOSS_ABL_HRRING  // timing ablation only (may race): row-major plane as a ring of strip slots
+  uint16_t* Hr = K.hr + (size_t)((blockIdx.y * gridDim.x + blockIdx.x) % ACOSS_ABL_HRRING) * kSR * ldr;
+#else
   uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
+#endif
+#ifdef ACOSS_ABL_HCRING  // timing ablation only (wrong results): strip-major plane as a ring of pairs
+  uint16_t* Hc = K.hc + (size_t)(p % ACOSS_ABL_HCRING) * kstride;
+#else
   uint16_t* Hc = K.hc + (size_t)p * kstride;
+#endif
   const float* X2b = V.X2 + (size_t)i0 * 24;
   const float* Nq0 = V.NXq + i0;
   auto nqr = [&](int r) {  // row norm: a scalar load at a compile-time offset
@@ -1213,7 +1221,12 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
   Hint hint{kNoHint, 1.0f};
   // the next row's line is loaded while this one is searched (its latency hidden)
   auto load_row = [&](LT& Ld, int i) {
+#ifdef ACOSS_ABL_HRRING
+    int64_t rowoff = (int64_t)((blockIdx.y * gridDim.x + blockIdx.x) % ACOSS_ABL_HRRING) * kSR * ldr +
+                     (int64_t)(i - i0) * ldr;
+#else
     int64_t rowoff = (int64_t)p * kstride + (int64_t)i * ldr;
+#endif
     asm volatile("" : "+s"(rowoff));  // per-row address: nothing per lane hoisted out of the loop
     if constexpr (KQ == 0) {
       Ld.template load_lanes<false>(K.hr + rowoff, 32, V.Np);
@@ -1366,7 +1379,11 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
   Hint hint{kNoHint, 1.0f};
   // the next column's line is loaded while this one is searched (its HBM latency hidden)
   auto load_col = [&](LT& Ld, int j) {
+#ifdef ACOSS_ABL_HCRING
+    int64_t coloff = (int64_t)(p % ACOSS_ABL_HCRING) * kstride + (int64_t)j * kSR;
+#else
     int64_t coloff = (int64_t)p * kstride + (int64_t)j * kSR;
+#endif
     asm volatile("" : "+s"(coloff));  // per-column address: nothing per lane hoisted out of the loop
     if constexpr (KQ == 0) {
       Ld.template load_lanes<true>(K.hc + coloff, (size_t)ldc * kSR, V.Mp);

@@ -66,41 +66,84 @@ __device__ int simple_oti_index(const double* pa, const double* pb) {
   return best;
 }
 
-// per-track chroma profile (sum over time, sequential), per-frame squared norms (fma chain),
-// the frame-major doubled copy ext[t][x][0..23], and the L-window norms of the unrolled track
+// Per-track scratch is packed by the tracks' own lengths and only for the tracks the call's pairs
+// name: k_simple_mark flags them, k_simple_scan gives each flagged track its frame offset toff[t]
+// (lengths rounded up to 8 frames) and the total, which sizes the workspace.
+__global__ void k_simple_mark(const int32_t* __restrict__ pairs, int64_t n_pairs, int32_t* __restrict__ used) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_pairs) {
+    used[pairs[2 * p]] = 1;
+    used[pairs[2 * p + 1]] = 1;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_simple_scan(const int32_t* __restrict__ len, const int32_t* __restrict__ used,
+                                                      int n_tracks, int64_t* __restrict__ toff,
+                                                      int64_t* __restrict__ total) {
+  __shared__ int64_t wsum[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int per = (n_tracks + 1023) / 1024;
+  const int a = min(n_tracks, t * per), b = min(n_tracks, a + per);
+  int64_t mine = 0;
+  for (int u = a; u < b; ++u) mine += used[u] ? (int64_t)align_up((size_t)len[u], 8) : 0;
+  // inclusive scan of the per-thread sums: within the wave, then across the 16 waves
+  int64_t x = mine;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int64_t before = 0;
+  for (int v = 0; v < w; ++v) before += wsum[v];
+  int64_t run = before + x - mine;  // exclusive prefix of this thread
+  for (int u = a; u < b; ++u) {
+    toff[u] = used[u] ? run : -1;
+    run += used[u] ? (int64_t)align_up((size_t)len[u], 8) : 0;
+  }
+  if (t == 1023) *total = run;
+}
+
+// per flagged track: chroma profile (sum over time, sequential), per-frame squared norms (fma
+// chain), the L-window norms of the unrolled track, and (fast path) the frame-major doubled
+// query copy ext[x][0..23] and the 128-B reference records rec[x][0..15]
 __global__ void k_simple_track(const double* __restrict__ feats, const int64_t* __restrict__ off,
                                const int32_t* __restrict__ len, int n_tracks, int L, double* __restrict__ prof,
                                double* __restrict__ fnorm, double* __restrict__ wnorm, double* __restrict__ ext,
-                               double* __restrict__ rec, int64_t ldf) {
+                               double* __restrict__ rec, const int64_t* __restrict__ toff, int copies) {
   const int tr = blockIdx.x;
-  if (tr >= n_tracks) return;
+  if (tr >= n_tracks || toff[tr] < 0) return;
   const double* S = feats + off[tr];
   const int n = len[tr];
   const int t = threadIdx.x;
+  const int64_t o = toff[tr];
   if (t < 12) {
     double acc = 0.0;
     for (int x = 0; x < n; ++x) acc = acc + S[(size_t)t * n + x];
     prof[tr * 12 + t] = acc;
   }
-  double* E = ext + (size_t)tr * ldf * kExt;
-  double* R = rec + (size_t)tr * ldf * kRec;
+  double* E = ext + (size_t)o * kExt;
+  double* R = rec + (size_t)o * kRec;
   for (int x = t; x < n; x += blockDim.x) {
     double acc = 0.0;
     for (int d = 0; d < 12; ++d) {
       const double v = S[(size_t)d * n + x];
       acc = d == 0 ? v * v : fma(v, v, acc);
-      E[(size_t)x * kExt + d] = v;
-      E[(size_t)x * kExt + 12 + d] = v;
-      R[(size_t)x * kRec + d] = v;
+      if (copies) {
+        E[(size_t)x * kExt + d] = v;
+        E[(size_t)x * kExt + 12 + d] = v;
+        R[(size_t)x * kRec + d] = v;
+      }
     }
-    for (int d = 12; d < kRec; ++d) R[(size_t)x * kRec + d] = 0.0;
-    fnorm[(size_t)tr * ldf + x] = acc;
+    if (copies)
+      for (int d = 12; d < kRec; ++d) R[(size_t)x * kRec + d] = 0.0;
+    fnorm[o + x] = acc;
   }
   __syncthreads();
   for (int i = t; i + L <= n; i += blockDim.x) {
     double acc = 0.0;
-    for (int u = 0; u < L; ++u) acc = acc + fnorm[(size_t)tr * ldf + i + u];
-    wnorm[(size_t)tr * ldf + i] = acc;
+    for (int u = 0; u < L; ++u) acc = acc + fnorm[o + i + u];
+    wnorm[o + i] = acc;
   }
 }
 
@@ -108,7 +151,8 @@ __global__ void k_simple_track(const double* __restrict__ feats, const int64_t* 
 __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ feats, const int64_t* __restrict__ off,
                                                      const int32_t* __restrict__ len, const int32_t* __restrict__ pairs,
                                                      const double* __restrict__ prof, const double* __restrict__ wnorm,
-                                                     int64_t ldf, int L, int apply_oti, double* __restrict__ score,
+                                                     const int64_t* __restrict__ toff, int L, int apply_oti,
+                                                     double* __restrict__ score,
                                                      int32_t* __restrict__ oti_out) {
   __shared__ double sa[kMaxLen];
   __shared__ double sb[kMaxLen];
@@ -132,7 +176,7 @@ __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ 
     return;
   }
   for (int i = t; i < P; i += 256) {
-    sa[i] = wnorm[(size_t)ta * ldf + i];
+    sa[i] = wnorm[toff[ta] + i];
     mpk[i] = ~0ull;
   }
   __syncthreads();
@@ -140,7 +184,7 @@ __global__ __launch_bounds__(256) void k_simple_pair(const double* __restrict__ 
   int rowA[12];  // reference bin j pairs with query bin (j + k) mod 12
 #pragma unroll
   for (int c = 0; c < 12; ++c) rowA[c] = ((c + k) % 12) * na;
-  for (int j = t; j < Q; j += 256) sb[j] = wnorm[(size_t)tb * ldf + j];  // a roll keeps the norms
+  for (int j = t; j < Q; j += 256) sb[j] = wnorm[toff[tb] + j];  // a roll keeps the norms
   __syncthreads();
   for (int dg = t; dg < P + Q - 1; dg += 256) {
     const int o = dg - (P - 1);  // j - i
@@ -245,7 +289,8 @@ __device__ __forceinline__ double dpp_shl1_f64(double old, double v) {
 template <int K, int RED, int SH = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_simple_diag(const double* __restrict__ ext, const double* __restrict__ rec, const int32_t* __restrict__ len,
                                                      const int32_t* __restrict__ pairs, const double* __restrict__ prof,
-                                                     const double* __restrict__ wnorm, int64_t ldf, int n2max,
+                                                     const double* __restrict__ wnorm,
+                                                     const int64_t* __restrict__ toff, int n2max,
                                                      int sboff, int slotsz, int rboff, int ppb, int64_t n_pairs,
                                                      int apply_oti, double* __restrict__ score,
                                                      int32_t* __restrict__ oti_out) {
@@ -274,11 +319,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
   __syncthreads();
   const int kq = live ? __builtin_amdgcn_readfirstlane(s_k[slot]) : 0;  // query bin offset of the OTI pairing
-  const double* Ea = ext + (size_t)ta * ldf * kExt + kq;
-  const double* Eb = rec + (size_t)tb * ldf * kRec;
-  const double* Wa = wnorm + (size_t)ta * ldf;
+  const int64_t oa = live ? toff[ta] : 0, ob = live ? toff[tb] : 0;
+  const double* Ea = ext + (size_t)oa * kExt + kq;
+  const double* Eb = rec + (size_t)ob * kRec;
+  const double* Wa = wnorm + oa;
   // the reference's window norms (a roll keeps them) into LDS
-  for (int j = tl; live && j < Q; j += nthr) sb[j] = wnorm[(size_t)tb * ldf + j];
+  for (int j = tl; live && j < Q; j += nthr) sb[j] = wnorm[ob + j];
   __syncthreads();
   const int n2 = n2max;
   for (int i = tl; i < n2; i += nthr) mpk[i] = ~0ull;
@@ -447,25 +493,51 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
   if (n_pairs == 0) return ACOSS_OK;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   prof_begin(PH_SIMPLE, s);
-  const int64_t ldf = (int64_t)align_up((size_t)max(max_len, 1), 64);
-  const size_t prof_bytes = align_up((size_t)n_tracks * 12 * 8, 256);
-  const size_t vec_bytes = (size_t)n_tracks * ldf * 8;
-  // vec_bytes is a multiple of 512 (ldf % 64 == 0): every section stays 128-B aligned
-  const size_t bytes = prof_bytes + 2 * vec_bytes + vec_bytes * kExt + vec_bytes * kRec;
-  char* ws = static_cast<char*>(workspace(8, bytes));
-  if (!ws) return ACOSS_E_HIP;
-  double* prof = reinterpret_cast<double*>(ws);
-  double* fnorm = reinterpret_cast<double*>(ws + prof_bytes);
-  double* wnorm = reinterpret_cast<double*>(ws + prof_bytes + vec_bytes);
-  double* ext = reinterpret_cast<double*>(ws + prof_bytes + 2 * vec_bytes);
-  double* rec = reinterpret_cast<double*>(ws + prof_bytes + 2 * vec_bytes + vec_bytes * kExt);
-  hipLaunchKernelGGL(k_simple_track, dim3(n_tracks), dim3(256), 0, s, feats, track_off, track_len, n_tracks, sslen,
-                     prof, fnorm, wnorm, ext, rec, ldf);
-  ACOSS_LAUNCH_CHECK();
+  // kernel choice first: the per-track query / reference copies exist only for the fast path
   const char* kenv = getenv("ACOSS_SIMPLE_K");
   // K = 4 with DPP frame passing for long tracks (2000 frames: 133.5k pairs/s vs 101.3k for K = 5
-  // loading every frame), K = 5 for short ones (200 frames: 5.27M vs 5.11M)
-  const int kdiag = kenv ? atoi(kenv) : (max_len >= 512 ? 4 : 5);
+  // loading every frame), K = 5 for short ones (200 frames: 5.27M vs 5.11M); an override other
+  // than 2, 4 or 5 is ignored
+  int kdiag = max_len >= 512 ? 4 : 5;
+  if (kenv) {
+    const int v = atoi(kenv);
+    if (v == 2 || v == 4 || v == 5) kdiag = v;
+  }
+  const bool fast = sslen == kFastL;
+  const char* senv = getenv("ACOSS_SIMPLE_SH");
+  const int sh = senv ? atoi(senv) : 1;
+  // per-track tables (workspace slot 8): prof | toff | used | total; slot 13: fnorm, wnorm and, on
+  // the fast path, ext and rec, each packed by toff (the call's tracks only, at their own lengths:
+  // 336 B per frame on the fast path, 16 B otherwise)
+  const size_t prof_bytes = align_up((size_t)n_tracks * 12 * 8, 256);
+  const size_t toff_bytes = align_up((size_t)n_tracks * 8, 256);
+  const size_t used_bytes = align_up((size_t)n_tracks * 4, 256);
+  const size_t head = prof_bytes + toff_bytes + used_bytes + 256;
+  char* hd = static_cast<char*>(workspace(8, head));
+  if (!hd) return ACOSS_E_HIP;
+  double* prof = reinterpret_cast<double*>(hd);
+  int64_t* toff = reinterpret_cast<int64_t*>(hd + prof_bytes);
+  int32_t* used = reinterpret_cast<int32_t*>(hd + prof_bytes + toff_bytes);
+  int64_t* d_total = reinterpret_cast<int64_t*>(hd + prof_bytes + toff_bytes + used_bytes);
+  ACOSS_HIP_CHECK(hipMemsetAsync(used, 0, used_bytes, s));
+  hipLaunchKernelGGL(k_simple_mark, dim3((unsigned)((n_pairs + 255) / 256)), dim3(256), 0, s, pairs, n_pairs, used);
+  ACOSS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_simple_scan, dim3(1), dim3(1024), 0, s, track_len, used, n_tracks, toff, d_total);
+  ACOSS_LAUNCH_CHECK();
+  int64_t frames = 0;
+  ACOSS_HIP_CHECK(hipMemcpyAsync(&frames, d_total, 8, hipMemcpyDeviceToHost, s));
+  ACOSS_HIP_CHECK(hipStreamSynchronize(s));
+  const size_t vec_bytes = align_up((size_t)std::max<int64_t>(frames, 8) * 8, 256);
+  const size_t bytes = 2 * vec_bytes + (fast ? vec_bytes * (kExt + kRec) : 0);
+  char* ws = static_cast<char*>(workspace(13, bytes));
+  if (!ws) return ACOSS_E_HIP;
+  double* fnorm = reinterpret_cast<double*>(ws);
+  double* wnorm = reinterpret_cast<double*>(ws + vec_bytes);
+  double* ext = reinterpret_cast<double*>(ws + 2 * vec_bytes);
+  double* rec = reinterpret_cast<double*>(ws + 2 * vec_bytes + vec_bytes * kExt);
+  hipLaunchKernelGGL(k_simple_track, dim3(n_tracks), dim3(256), 0, s, feats, track_off, track_len, n_tracks, sslen,
+                     prof, fnorm, wnorm, ext, rec, toff, fast ? 1 : 0);
+  ACOSS_LAUNCH_CHECK();
   const int n2max = pow2_at_least(max(max_len - kFastL + 1, 2));
   const int sboff = n2max;
   const int slotsz = sboff + (int)align_up((size_t)max_len, 2);
@@ -479,9 +551,11 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
   if (ppb != 1 && ppb != 2 && ppb != 4) ppb = 1;
   while (ppb > 1 && (size_t)ppb * (n2max + align_up((size_t)max_len, 2)) * 8 > 96 * 1024) ppb /= 2;
   // row minima through LDS chunks for packed short pairs, per-step DPP minima for long ones
-  // (measured: 200 frames 5.85M vs 5.58M pairs/s, 2000 frames 48.0k vs 51.0k)
+  // (measured: 200 frames 5.85M vs 5.58M pairs/s, 2000 frames 48.0k vs 51.0k); the K = 5 and the
+  // frame-passing kernels always take the DPP minima, so they reserve no reduction buffer
   const char* renv = getenv("ACOSS_SIMPLE_RED");
-  const int red = renv ? atoi(renv) : (ppb > 1 ? 1 : 0);
+  const bool red_kernel = !(kdiag == 5 || (kdiag == 4 && sh));
+  const int red = red_kernel ? (renv ? atoi(renv) : (ppb > 1 ? 1 : 0)) : 0;
   const int rboff = ppb * slotsz;
   const size_t lds = ((size_t)rboff + (red ? (size_t)4 * U * kRbufStride : 0)) * 8;
   for (int64_t p0 = 0; p0 < n_pairs; p0 += (int64_t)ppb << 20) {
@@ -489,9 +563,7 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
     const int32_t* pp = pairs + 2 * p0;
     double* so = score_out + p0;
     int32_t* oo = oti_out ? oti_out + p0 : nullptr;
-    if (sslen == kFastL && (kdiag == 2 || kdiag == 4 || kdiag == 5)) {
-      const char* senv = getenv("ACOSS_SIMPLE_SH");
-      const int sh = senv ? atoi(senv) : 1;
+    if (fast) {
       auto kern = (kdiag == 4 && sh) ? k_simple_diag<4, 0, 1>
                   : kdiag == 5 ? k_simple_diag<5, 0>
                   : kdiag == 4 ? (red ? k_simple_diag<4, 1> : k_simple_diag<4, 0>)
@@ -500,10 +572,10 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
         ACOSS_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(kern, dim3((unsigned)((np + ppb - 1) / ppb)), dim3(256), lds, s, ext, rec, track_len, pp, prof,
-                         wnorm, ldf, n2max, sboff, slotsz, rboff, ppb, np, apply_oti, so, oo);
+                         wnorm, toff, n2max, sboff, slotsz, rboff, ppb, np, apply_oti, so, oo);
     } else {
       hipLaunchKernelGGL(k_simple_pair, dim3((unsigned)np), dim3(256), 0, s, feats, track_off, track_len, pp, prof,
-                         wnorm, ldf, sslen, apply_oti, so, oo);
+                         wnorm, toff, sslen, apply_oti, so, oo);
     }
     ACOSS_LAUNCH_CHECK();
   }

@@ -73,8 +73,10 @@ __global__ void k_snf_sort_knn(const int32_t* __restrict__ J, const double* __re
 // One launch sums a chunk of `cnt` matrices (the skipped one already left out, ascending m)
 // onto the running sum `part` (untransposed; NULL for the first chunk). A chunk that is not
 // the last writes the running sum to `part_out` untransposed; the last divides and writes At.
+// A middle chunk reads and writes the same running sum (part == part_out): each element is read
+// and then written by the same thread, and the two pointers are not __restrict__.
 __global__ __launch_bounds__(256) void k_snf_avg_t(MatPtrs mats, int32_t cnt, int32_t n, double denom,
-                                                   const double* __restrict__ part, double* __restrict__ part_out,
+                                                   const double* part, double* part_out,
                                                    double* __restrict__ At) {
   __shared__ double tile[64][65];
   const int a0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
@@ -187,7 +189,7 @@ using namespace acoss;
 
 extern "C" int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t skip, int32_t n,
                               const int32_t* J, const double* V, int32_t K, double reg_diag, double* out,
-                              void* hip_stream) {
+                              int32_t validate, void* hip_stream) {
   clear_error();
   if (!mats || n_mats < 2 || skip < 0 || skip >= n_mats || n <= 0 || !J || !V || !out || K <= 0 ||
       K > kSnfMaxK || K > n) {
@@ -215,13 +217,17 @@ extern "C" int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t
   ACOSS_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
   hipLaunchKernelGGL(k_snf_sort_knn, dim3((n + 255) / 256), dim3(256), 0, s, J, V, n, K, Js, Vs, d_err);
   ACOSS_LAUNCH_CHECK();
-  // the kNN columns are checked before any product reads a row they name
-  int h_err = 0;
-  ACOSS_HIP_CHECK(hipMemcpyAsync(&h_err, d_err, 4, hipMemcpyDeviceToHost, s));
-  ACOSS_HIP_CHECK(hipStreamSynchronize(s));
-  if (h_err) {
-    set_error("acoss_snf_step: kNN column indices must lie in [0, %d) without repeats within a row", n);
-    return ACOSS_E_ARG;
+  // validate: the kNN columns are checked (one stream sync) before any product reads a row they
+  // name. Without it a bad row has already been made harmless (its own column, weight 0), so no
+  // kernel reads outside the matrices; a caller that validated J once per fusion skips the sync.
+  if (validate) {
+    int h_err = 0;
+    ACOSS_HIP_CHECK(hipMemcpyAsync(&h_err, d_err, 4, hipMemcpyDeviceToHost, s));
+    ACOSS_HIP_CHECK(hipStreamSynchronize(s));
+    if (h_err) {
+      set_error("acoss_snf_step: kNN column indices must lie in [0, %d) without repeats within a row", n);
+      return ACOSS_E_ARG;
+    }
   }
   // average of the other matrices, ascending m, in chunks of kSnfChunk pointers; the running
   // sum of a multi-chunk average lives in Bm (free until the first product)

@@ -127,9 +127,11 @@ int acoss_wcsm(const float* CSM, int32_t M, int32_t N, int32_t k1, int32_t k2, f
  * checked on the device before any product runs. mats: HOST array of n_mats device pointers
  * to (n x n) float64 matrices; out (n x n) float64 may alias mats[skip] but no other.
  * n_mats >= 2 (any number; more than 16 others are averaged in passes), 0 < K <= min(n, 64).
- * Synchronises the stream once (the index check). */
+ * validate = 1: the index check synchronises the stream once and a bad J returns ACOSS_E_ARG;
+ * validate = 0 (J already checked, e.g. once per fusion): no sync, and a bad row is replaced by
+ * a weight-0 entry on its own column, so no kernel reads outside the matrices. */
 int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t skip, int32_t n, const int32_t* J,
-                   const double* V, int32_t K, double reg_diag, double* out, void* hip_stream);
+                   const double* V, int32_t K, double reg_diag, double* out, int32_t validate, void* hip_stream);
 
 /* SiMPle matrix profile score (A11, acoss/algorithms/simple_silva.py:68-118) for a batch of
  * ordered pairs, including the per-pair OTI roll of the reference (Simple.oti, :45-54).

@@ -1,0 +1,89 @@
+"""EarlyFusion's beat-synchronous block features on the host (f3, earlyfusion_traile.py:67-154,
+214-247), CPU only.
+
+The reference resizes each beat block with skimage.transform.resize(x, (frames_per_block, d),
+anti_aliasing=True, mode='constant'); skimage is absent here, so acoss's resize_block restates it
+with scipy.ndimage. This test pins that restatement against a second, independent restatement of
+skimage's published algorithm written with plain numpy loops (Gaussian pre-filter, sigma =
+max(0, (factor - 1) / 2), kernel radius int(4 sigma + 0.5), zero padding; then linear
+interpolation at input coordinate (k + 0.5) * factor - 0.5 with zeros outside the block, i.e.
+ndimage.zoom(grid_mode=True, mode='grid-constant')). Both are restatements: parity with skimage
+itself stays unpinned. The SSM feature is pinned against the reference's get_ssm (np_oracle,
+golden-pinned) taken on the upper triangle, and the block layout against the reference's loop.
+"""
+import numpy as np
+import pytest
+
+from oracle import np_oracle as npo
+
+
+def _gauss_kernel(sigma):
+    r = int(4.0 * sigma + 0.5)
+    x = np.arange(-r, r + 1, dtype=np.float64)
+    w = np.exp(-0.5 * x * x / (sigma * sigma))
+    return w / w.sum(), r
+
+
+def _resize_direct(x, n_out):
+    x = np.asarray(x, np.float64)
+    n_in, d = x.shape
+    factor = n_in / float(n_out)
+    sigma = max(0.0, (factor - 1.0) / 2.0)
+    if sigma > 0:
+        w, r = _gauss_kernel(sigma)
+        f = np.zeros_like(x)
+        for i in range(n_in):
+            for t in range(-r, r + 1):
+                if 0 <= i + t < n_in:
+                    f[i] += w[t + r] * x[i + t]
+    else:
+        f = x.copy()
+    out = np.zeros((n_out, d))
+    for k in range(n_out):
+        c = (k + 0.5) * factor - 0.5
+        i0 = int(np.floor(c))
+        a = c - i0
+        lo = f[i0] if 0 <= i0 < n_in else 0.0
+        hi = f[i0 + 1] if 0 <= i0 + 1 < n_in else 0.0
+        out[k] = (1 - a) * lo + a * hi
+    return out
+
+
+@pytest.mark.parametrize("n_in,n_out", [(120, 50), (50, 50), (37, 50), (400, 40), (41, 40), (12, 40)])
+def test_resize_block_matches_direct_restatement(n_in, n_out):
+    from acoss.algorithms.earlyfusion_traile import resize_block
+    rng = np.random.default_rng(n_in * 7 + n_out)
+    X = rng.normal(size=(n_in + 30, 20)).astype(np.float32)
+    got = resize_block(X, 10, 10 + n_in, n_out)
+    np.testing.assert_allclose(got, _resize_direct(X[10:10 + n_in], n_out), rtol=1e-12, atol=1e-12)
+
+
+def test_block_features_match_reference_loop(tmp_path):
+    """load_features' MFCC / SSM / chroma blocks vs the reference's loop (:107-126) built from
+    the pinned pieces: resize (restated above), z-normalisation, get_ssm upper triangle."""
+    from acoss import synthetic
+    from acoss.algorithms.earlyfusion_traile import EarlyFusion
+    rng = np.random.default_rng(3)
+    tracks = [np.abs(rng.normal(size=(900, 12))).astype(np.float32)]
+    csv, fdir = synthetic.write_feature_dataset(str(tmp_path), tracks, np.array([0]), with_mfcc=True)
+    ef = EarlyFusion(csv, fdir, shortname="t", cachedir=str(tmp_path / "cache"))
+    bf = ef.load_features(0)
+    from acoss.features_io import load_features
+    raw = load_features(fdir + "W00000/T000000.h5")
+    mfcc = np.array(raw["mfcc_htk"]).T
+    onsets = raw["madmom_features"]["onsets"]
+    nb = len(onsets) - ef.blocksize
+    assert bf["mfccs"].shape == (nb, 50 * 20) and bf["ssms"].shape == (nb, 1225) and bf["chromas"].shape == (nb, 480)
+    pix = np.arange(50)
+    I, J = np.meshgrid(pix, pix)
+    for b in range(nb):
+        x = _resize_direct(mfcc[onsets[b]:onsets[b + ef.blocksize - 1]], 50)
+        x -= np.mean(x, 0)[None, :]
+        xnorm = np.sqrt(np.sum(x ** 2, 1))[:, None]
+        xnorm[xnorm == 0] = 1
+        xn = x / xnorm
+        np.testing.assert_allclose(bf["mfccs"][b], xn.flatten().astype(np.float32), rtol=2e-6, atol=1e-7)
+        np.testing.assert_allclose(bf["ssms"][b], npo.get_ssm(xn)[I < J].astype(np.float32), rtol=2e-6, atol=2e-6)
+        c = _resize_direct(tracks[0][onsets[b]:onsets[b + ef.blocksize]], 40)
+        np.testing.assert_allclose(bf["chromas"][b], c.flatten().astype(np.float32), rtol=2e-6, atol=1e-7)
+    np.testing.assert_array_equal(bf["chroma_med"], np.median(tracks[0], axis=0))

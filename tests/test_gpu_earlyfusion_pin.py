@@ -1,0 +1,151 @@
+"""EarlyFusion end to end against the numpy oracle composition (A15, GPU).
+
+EarlyFusion.similarity (acoss/algorithms/earlyfusion_traile.py:157-198) composes three CSMs
+(float32 BLAS in the reference, MFMA here), a kappa-NN row binarisation, getWCSM and four
+constrained Smith-Waterman alignments. In general the CSMs of the two paths differ in float32
+summation order, so a row whose kappa-th and (kappa+1)-th smallest values are within a few ulps
+could binarise differently. The block features here are built so that every CSM is EXACT in
+any summation order: small-integer MFCC / SSM blocks (every |x|^2, x.y and d^2 is an integer
+below 2^24; sqrt correctly rounded on both sides) and 0/1 chroma blocks with exactly 16 ones
+(norm 4, so the normalised rows and their dot products are exact binary fractions). Both paths
+then see bit-identical CSMs, resolve ties by the same lowest-column rule (acoss_binarize_rows,
+np_oracle.csm_to_binary), and the three per-feature scores must be EQUAL to the oracle's.
+
+The early-fusion matrix exp(-sum getWCSM) cannot be exact: getWCSM averages the k smallest
+values in numpy's np.partition order, which is not reproducible. Its score is asserted equal
+on every pair whose float64 early matrix is separated at the kappa-NN boundary by more than
+EARLY_MARGIN relative (float32 rounding of the mean/exp chain is ~1e-6), and at least 70 % of
+the pairs must be such pairs. The late / early+late SNF outputs (:200-206) must match
+np_oracle.snf_fused of the ORACLE's matrices at the SNF float32 tolerance of test_gpu_plugin.py.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from oracle import np_oracle as npo
+from acoss import synthetic
+
+pytestmark = pytest.mark.gpu
+
+N_TRACKS = 24          # SNF with K = 20 needs more than 21 songs
+EARLY_MARGIN = 5e-6   # ~5x the float32 error of the getWCSM mean / exp chain
+
+
+def _clique_blocks(rng, nb):
+    """Integer-exact block features of one clique's base song."""
+    return {"mfccs": rng.integers(-2, 3, size=(nb, 1000)).astype(np.float32),
+            "ssms": rng.integers(0, 4, size=(nb, 1225)).astype(np.float32),
+            "chromas": _chroma_rows(rng, nb)}
+
+
+def _chroma_rows(rng, nb):
+    X = np.zeros((nb, 480), np.float32)
+    for b in range(nb):
+        X[b, rng.choice(480, 16, replace=False)] = 1.0
+    return X
+
+
+def _cover(rng, base, nb):
+    """A cover: the base's blocks from a random start, resampled to nb blocks, with integer
+    perturbations (still exact) and a few chroma ones moved."""
+    n0 = len(base["mfccs"])
+    idx = np.minimum((np.arange(nb) * (n0 / nb) + rng.integers(0, 5)).astype(np.int64), n0 - 1)
+    out = {}
+    out["mfccs"] = np.clip(base["mfccs"][idx] + rng.integers(-1, 2, size=(nb, 1000)) * (rng.random((nb, 1000)) < 0.3),
+                           -2, 2).astype(np.float32)
+    out["ssms"] = np.clip(base["ssms"][idx] + rng.integers(-1, 2, size=(nb, 1225)) * (rng.random((nb, 1225)) < 0.3),
+                          0, 3).astype(np.float32)
+    ch = base["chromas"][idx].copy()
+    for b in range(nb):
+        if rng.random() < 0.5:
+            on, off = np.flatnonzero(ch[b] == 1), np.flatnonzero(ch[b] == 0)
+            ch[b, rng.choice(on, 4, replace=False)] = 0
+            ch[b, rng.choice(off, 4, replace=False)] = 1
+    out["chromas"] = ch
+    return out
+
+
+def _boundary_margin(D, nn):
+    s = np.sort(D.astype(np.float64), 1)
+    gap = s[:, nn] - s[:, nn - 1]
+    return float(np.min(gap / np.maximum(np.abs(s[:, nn]), 1e-12)))
+
+
+def _oracle_pair(f1, f2, kappa, K):
+    C = {"mfccs": npo.get_csm(f1["mfccs"], f2["mfccs"]), "ssms": npo.get_csm(f1["ssms"], f2["ssms"]),
+         "chromas": npo.get_csm_blocked_oti(f1["chromas"], f2["chromas"], f1["chroma_med"], f2["chroma_med"],
+                                           npo.get_csm_cosine)}
+    W = np.zeros_like(C["mfccs"])
+    for s in ("mfccs", "ssms", "chromas"):
+        W += npo.getWCSM(C[s], K, K)
+    E = np.exp(-W)
+    mats = [C["mfccs"], C["ssms"], C["chromas"], E]
+    return mats, [oracle.sw_constrained(npo.csm_to_binary(M, kappa)) for M in mats]
+
+
+@pytest.fixture(scope="module")
+def corpus(tmp_path_factory):
+    root = tmp_path_factory.mktemp("efpin")
+    rng = np.random.Generator(np.random.PCG64(2024))
+    feats, labels = [], []
+    for c in range(N_TRACKS // 2):
+        base = _clique_blocks(rng, int(rng.integers(40, 90)))
+        for v in range(2):
+            bf = dict(base) if v == 0 else _cover(rng, base, int(rng.integers(40, 90)))
+            # integer medians (exact in float32): the blocked-OTI roll varies by pair
+            bf["chroma_med"] = rng.permutation(12).astype(np.float32)
+            feats.append(bf)
+            labels.append(c)
+    # per-track input files only carry the clique labels; the block features go straight into
+    # the plugin's per-track cache ('<prefix>_<i>.h5' -> .npz twin), as load_features reads them
+    tracks = [np.zeros((8, 12), np.float32) for _ in range(N_TRACKS)]
+    csv, fdir = synthetic.write_feature_dataset(str(root), tracks, np.asarray(labels))
+    return root, csv, fdir, feats
+
+
+def test_earlyfusion_scores_equal_oracle(corpus, monkeypatch):
+    from acoss.algorithms.earlyfusion_traile import EarlyFusion
+    from acoss.features_io import save_features
+    root, csv, fdir, feats = corpus
+    monkeypatch.chdir(root)
+    ef = EarlyFusion(csv, fdir, shortname="pin", cachedir=str(root / "cache"))
+    for i, bf in enumerate(feats):
+        save_features("%s_%i.h5" % (ef.get_cacheprefix(), i), bf)
+    ef.all_pairwise(symmetric=True)
+    keys = ["mfccs", "ssms", "chromas", "early"]
+    ref = {k: np.zeros((N_TRACKS, N_TRACKS), np.float32) for k in keys}
+    safe = np.zeros((N_TRACKS, N_TRACKS), bool)
+    otis = set()
+    for i in range(N_TRACKS):
+        for j in range(i + 1, N_TRACKS):
+            mats, scores = _oracle_pair(feats[i], feats[j], ef.kappa, ef.K)
+            nn = npo.nneighbs(ef.kappa, mats[0].shape[1])
+            safe[i, j] = safe[j, i] = _boundary_margin(mats[3], nn) > EARLY_MARGIN
+            otis.add(npo.get_oti(feats[i]["chroma_med"], feats[j]["chroma_med"]))
+            for k, v in zip(keys, scores):
+                ref[k][i, j] = v
+    assert len(otis) >= 6  # the roll is exercised
+    npairs = N_TRACKS * (N_TRACKS - 1) // 2
+    assert np.triu(safe, 1).sum() >= 0.7 * npairs
+    for k in keys:
+        ref[k] += ref[k].T
+        assert np.count_nonzero(ref[k]) > npairs
+        got = np.asarray(ef.Ds[k])
+        if k == "early":
+            np.testing.assert_array_equal(got[safe], ref[k][safe], err_msg=k)
+        else:
+            np.testing.assert_array_equal(got, ref[k], err_msg=k)
+    # covers score above non-covers (the inputs carry real structure)
+    lab = np.arange(N_TRACKS) // 2
+    same = (lab[:, None] == lab[None, :]) & ~np.eye(N_TRACKS, dtype=bool)
+    assert ref["mfccs"][same].mean() > 2 * ref["mfccs"][~same & ~np.eye(N_TRACKS, dtype=bool)].mean()
+    # late fusion of the ORACLE's matrices (not the GPU's) at the SNF float32 tolerance; early+late
+    # takes the GPU's early matrix (equal to the oracle's on the separated pairs) with the
+    # oracle's three others
+    early_gpu = np.array(ef.Ds["early"])
+    late = npo.snf_fused([1.0 / (1.0 + ref[s]) for s in ["chromas", "ssms", "mfccs"]], K=20, niters=20)
+    el = npo.snf_fused([1.0 / (1.0 + m) for m in (ref["chromas"], ref["ssms"], ref["mfccs"], early_gpu)], K=20,
+                       niters=20)
+    ef.do_late_fusion()
+    np.testing.assert_allclose(np.asarray(ef.Ds["late"]), late, rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(np.asarray(ef.Ds["early+late"]), el, rtol=1e-5, atol=1e-9)

@@ -268,9 +268,14 @@ def test_snf_step_rejects_bad_args():
     for Jbad in (Jb, Jd, np.full((8, 2), 1 << 20, np.int32)):
         Jt = torch.as_tensor(Jbad).cuda()
         rc = lib.acoss_snf_step(ptrs, 2, 0, 8, ctypes.c_void_p(Jt.data_ptr()), ctypes.c_void_p(Vd.data_ptr()), 2,
-                                1.0, ctypes.c_void_p(out.data_ptr()), _lib._stream())
+                                1.0, ctypes.c_void_p(out.data_ptr()), 1, _lib._stream())
         assert rc == -1 and b"kNN column" in lib.acoss_last_error()
+        # unvalidated: no error code, and the bad row is harmless (no read outside the matrices)
+        rc = lib.acoss_snf_step(ptrs, 2, 0, 8, ctypes.c_void_p(Jt.data_ptr()), ctypes.c_void_p(Vd.data_ptr()), 2,
+                                1.0, ctypes.c_void_p(out.data_ptr()), 0, _lib._stream())
+        assert rc == 0
+        torch.cuda.synchronize()
     Jt = torch.as_tensor(J).cuda()
     rc = lib.acoss_snf_step(ptrs, 2, 0, 8, ctypes.c_void_p(Jt.data_ptr()), ctypes.c_void_p(Vd.data_ptr()), 2, 1.0,
-                            ctypes.c_void_p(out.data_ptr()), _lib._stream())
+                            ctypes.c_void_p(out.data_ptr()), 1, _lib._stream())
     assert rc == 0

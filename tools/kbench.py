@@ -24,9 +24,10 @@ ap.add_argument("--frames", type=int, default=2000)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--dmax", action="store_true")
 ap.add_argument("--noprof", action="store_true", help="no per-phase events: plain wall time per call")
+ap.add_argument("--corpus", choices=["hard", "bench"], default="hard")
 ap.add_argument("--mixed", default="", help="LO,HI: each track cut to a length drawn from [LO, HI] (HI <= frames)")
 a = ap.parse_args()
-tracks, labels = corpus_tracks(1, a.frames, 20250101)
+tracks, labels = corpus_tracks(1, a.frames, 20250101, a.corpus)
 if a.mixed:
     lo, hi = (int(v) for v in a.mixed.split(","))
     rng = np.random.Generator(np.random.PCG64(7))
