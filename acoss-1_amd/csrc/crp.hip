@@ -904,6 +904,9 @@ struct Stage {
   size_t sel_lds = 0, pan_lds = 0;
 };
 
+// Default slots per XCD of the row-major key-plane ring (ACOSS_HR_RING overrides; 0 = off).
+constexpr int kHrRingSlots = 0;
+
 int prepare_stage(int m, int ld, Stage* st) {
   st->R = pick_R(m, ld);
   if (st->R <= 0) {
@@ -1133,6 +1136,35 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
     w_kpl[b] = static_cast<void*>(carve(4 * (size_t)kstride * sub));
     w_rt[b] = reinterpret_cast<uint32_t*>(carve(4 * (size_t)mask_stride * sub));
   }
+  // row-major key plane as per-XCD rings of strip slots (HrRing, crp_split.hip): ACOSS_HR_RING =
+  // slots per XCD (a power of two; 0 = per-pair planes). One ring + its counters per stream.
+  HrRing rings[3] = {};
+  if (split) {
+    int S = kHrRingSlots;
+    if (const char* e = getenv("ACOSS_HR_RING")) S = atoi(e);
+    if (S < 0 || (S & (S - 1)) != 0 || S > 4096) S = kHrRingSlots;
+    if (S > 0) {
+      const size_t ring_elems = (size_t)8 * S * 32 * ldk;               // uint16
+      const size_t ctl_bytes = align_up((size_t)8 * 16 * 8 + (size_t)8 * S * 4, 256);
+      const size_t per = align_up(ring_elems * 2, 256) + ctl_bytes;
+      char* rw = static_cast<char*>(workspace(14, per * nbuf));
+      if (!rw) return ACOSS_E_HIP;
+      // the counters must start at zero, and again whenever the buffer or the slot count changes
+      static void* ctl_ptr[3] = {nullptr, nullptr, nullptr};
+      static int ctl_slots[3] = {0, 0, 0};
+      for (int b = 0; b < nbuf; ++b) {
+        char* base = rw + per * b;
+        char* ctl = base + align_up(ring_elems * 2, 256);
+        rings[b] = HrRing{reinterpret_cast<uint16_t*>(base), reinterpret_cast<unsigned long long*>(ctl),
+                          reinterpret_cast<unsigned*>(ctl + 8 * 16 * 8), S};
+        if (ctl_ptr[b] != ctl || ctl_slots[b] != S) {
+          ACOSS_HIP_CHECK(hipMemsetAsync(ctl, 0, ctl_bytes, s));
+          ctl_ptr[b] = ctl;
+          ctl_slots[b] = S;
+        }
+      }
+    }
+  }
   hipStream_t ss[3] = {s, s, s};
   for (int b = 1; split && b < nbuf; ++b) {
     ss[b] = side_stream(b - 1);
@@ -1168,7 +1200,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
         const int b = k % nst;
         CrpBatch Bs{feats, X2, track_off, track_len, NX, ldn, pb + 2 * s0, w_oti + s0, w_dims + s0, m, tau,
                     w_yrot + (size_t)s0 * yrot_stride, yrot_stride};
-        if ((rc = launch_crp_split(Bs, ns, L, params->kappa, w_kpl[b], ldk, kstride, w_rt[b],
+        if ((rc = launch_crp_split(Bs, ns, L, params->kappa, w_kpl[b], rings[b], ldk, kstride, w_rt[b],
                                    w_thr_r + (size_t)s0 * thr_stride, w_T_r + (size_t)s0 * thr_stride,
                                    w_thr_c + (size_t)s0 * thr_stride, w_T_c + (size_t)s0 * thr_stride, thr_stride,
                                    w_mask + (size_t)s0 * mask_stride, mask_stride, ld, ss[b])))

@@ -87,6 +87,7 @@ constexpr int kSR = 32;                       // rows per strip
 struct KeyPlanes {
   uint16_t* hr;
   uint16_t* hc;
+  HrRing ring;
 };
 
 // Exact key of cell (i, j), recomputed in the sweep's canonical order: 12-term fmaf chain per
@@ -180,17 +181,12 @@ __device__ __forceinline__ float dpp_shr1(float v) {  // lane l <- lane l - 1 (l
 // branch-free emit.
 template <bool PARTIAL>
 __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr,
-                                               int ldc, int64_t kstride) {
+                                               int ldc, int64_t kstride, uint16_t* Hr) {
   constexpr int kSteps = kSR + kMS - 1;  // 40
   const int i0 = strip * kSR;
   const int rows = PARTIAL ? min(kSR, V.Mp - i0) : kSR;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#ifdef ACOSS_ABL_HRRING  // timing ablation only (may race): row-major plane as a ring of strip slots
-  uint16_t* Hr = K.hr + (size_t)((blockIdx.y * gridDim.x + blockIdx.x) % ACOSS_ABL_HRRING) * kSR * ldr;
-#else
-  uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
-#endif
 #ifdef ACOSS_ABL_HCRING  // timing ablation only (wrong results): strip-major plane as a ring of pairs
   uint16_t* Hc = K.hc + (size_t)(p % ACOSS_ABL_HCRING) * kstride;
 #else
@@ -1209,8 +1205,8 @@ struct LineOf<2> {
 };
 
 template <int NW, int KQ, int RB>
-__device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, const KeyPlanes& K, int ldr,
-                                          int64_t kstride, float kappa, float* __restrict__ thr,
+__device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, const uint16_t* Hr, int ldr,
+                                          float kappa, float* __restrict__ thr,
                                           float* __restrict__ Tq, int64_t thr_stride, uint32_t* __restrict__ RT,
                                           int64_t rt_stride, int ld, WaveLds* wl, uint32_t (*rowbits)[RB]) {
   using LT = typename LineOf<KQ>::T;
@@ -1221,20 +1217,15 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
   Hint hint{kNoHint, 1.0f};
   // the next row's line is loaded while this one is searched (its latency hidden)
   auto load_row = [&](LT& Ld, int i) {
-#ifdef ACOSS_ABL_HRRING
-    int64_t rowoff = (int64_t)((blockIdx.y * gridDim.x + blockIdx.x) % ACOSS_ABL_HRRING) * kSR * ldr +
-                     (int64_t)(i - i0) * ldr;
-#else
-    int64_t rowoff = (int64_t)p * kstride + (int64_t)i * ldr;
-#endif
+    int64_t rowoff = (int64_t)(i - i0) * ldr;
     asm volatile("" : "+s"(rowoff));  // per-row address: nothing per lane hoisted out of the loop
     if constexpr (KQ == 0) {
-      Ld.template load_lanes<false>(K.hr + rowoff, 32, V.Np);
+      Ld.template load_lanes<false>(Hr + rowoff, 32, V.Np);
     } else if constexpr (KQ == 2) {
-      Ld.A.template load_lanes<false>(K.hr + rowoff, 32, V.Np);
-      Ld.B.template load_lanes<false>(K.hr + rowoff + 2048, 32, V.Np - 2048);
+      Ld.A.template load_lanes<false>(Hr + rowoff, 32, V.Np);
+      Ld.B.template load_lanes<false>(Hr + rowoff + 2048, 32, V.Np - 2048);
     } else {
-      const uint16_t* row = K.hr + rowoff;
+      const uint16_t* row = Hr + rowoff;
       Ld.load([&](int e) { return row + (unsigned)e; }, V.Np);
     }
   };
@@ -1322,10 +1313,30 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
   const PairView V = pair_view(B, p);
   const int strip = blockIdx.x, i0 = strip * kSR;
   if (i0 >= V.Mp || V.Np <= 0) return;
+  // the strip's row-major plane: per pair, or a slot of this XCD's ring (HrRing)
+  __shared__ int s_slot;
+  uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
+  if (K.ring.slots) {
+    if (threadIdx.x == 0) {
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+      const unsigned long long t = atomicAdd(K.ring.ticket + 16 * xcc, 1ull);
+      const unsigned S = (unsigned)K.ring.slots;
+      const int slot = (int)(xcc * S + (unsigned)(t & (S - 1)));
+      const unsigned g = (unsigned)(t / S);
+      // the previous owner (ticket t - S of this XCD) started earlier and is resident or done;
+      // the acquire also invalidates this CU's L1 (stale lines of an earlier owner here)
+      while (__hip_atomic_load(K.ring.gen + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != g)
+        __builtin_amdgcn_s_sleep(2);
+      s_slot = slot;
+    }
+    __syncthreads();
+    Hr = K.ring.base + (size_t)__builtin_amdgcn_readfirstlane(s_slot) * kSR * ldr;  // wave-uniform (SGPR)
+  }
   if (i0 + kSR <= V.Mp)
-    sweep_body_sys<false>(V, p, strip, K, ldr, ldc, kstride);
+    sweep_body_sys<false>(V, p, strip, K, ldr, ldc, kstride, Hr);
   else
-    sweep_body_sys<true>(V, p, strip, K, ldr, ldc, kstride);
+    sweep_body_sys<true>(V, p, strip, K, ldr, ldc, kstride, Hr);
   ACOSS_STAMP(r0);
   __syncthreads();  // the strip's F rows are complete (block-scope visibility of the global stores)
 #ifdef ACOSS_ABL_NOROWS  // timing ablation only (wrong results): sweep without the row select
@@ -1334,13 +1345,17 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
   WaveLds* wl = reinterpret_cast<WaveLds*>(smem);
   uint32_t(*rowbits)[RB] = reinterpret_cast<uint32_t(*)[RB]>(smem + 4 * sizeof(WaveLds));
   if (KQ == 8 || (KQ != 16 && V.Np <= short_n))
-    rows_body<4, 8, RB>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+    rows_body<4, 8, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   else if (KQ == 16)  // (mixed launches leave it out: a third select in one kernel costs more than it saves)
-    rows_body<4, 16, RB>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+    rows_body<4, 16, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   else if (KQ == 2 && V.Np > 2048)
-    rows_body<4, 2, RB>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+    rows_body<4, 2, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   else
-    rows_body<4, 0, RB>(V, p, strip, K, ldr, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+    rows_body<4, 0, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+  if (K.ring.slots) {  // every wave's reads of the slot have returned: hand it to ticket t + S
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(K.ring.gen + s_slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   ACOSS_STAMP(r1);
   ACOSS_STAMP_ADD(4, r0, r1);  // row select
   if (threadIdx.x == 0) ACOSS_STAMP_ADD(5, 0ull, 1ull);
@@ -1485,12 +1500,13 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
 // kplanes: nb * kstride uint16 row-major prefixes, then nb * kstride uint16 strip-major ones;
 // RT: nb * mask_stride
 // words (same layout as maskT).
-int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, int ldk, int64_t kstride,
+int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, const HrRing& ring, int ldk,
+                     int64_t kstride,
                      uint32_t* RT, float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride,
                      uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s) {
   if (B.m != kMS || B.tau != 1 || L > 4096) return 1;
   const size_t plane = (size_t)nb * kstride;
-  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane};
+  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane, ring};
   const int nstrips = (L + kSR - 1) / kSR;
   // launches whose lines all fit 512 / 1024 codes take LineS<8> / LineS<16> throughout; in
   // mixed launches each pair picks per side (lines of <= short_n codes LineS<8>, past 2048

@@ -70,6 +70,55 @@ def log(msg):
 T_START = time.perf_counter()
 
 
+def cpu_share():
+    """Threads for the CPU baseline: the CPU share the GPU box grants one GPU (OMP_NUM_THREADS is
+    set to it there; nproc reports the whole machine), else the CPUs this process may run on."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        omp = 0
+    return max(1, min(n, omp) if omp > 0 else n)
+
+
+ORACLE_FIXTURE = os.path.join(ROOT, "tests", "golden", "bench_oracle_qmax.npz")
+
+
+def oracle_map_parity(tracks, labels, lens, pairs, Dfull, Dsym, frames, gpu_stats):
+    """The whole step against the oracle: the oracle's Qmax for every pair of this corpus
+    (tests/golden/make_bench_oracle.py; a full oracle step takes ~20 min on the box's 16-thread
+    share, so it is precomputed for this exact corpus), compared bit for bit with the GPU's, and
+    MR/MRR/MDR/MAP/Top-k of both finished matrices (algorithm_template.py:206-291)."""
+    from acoss import evaluation
+    if not os.path.exists(ORACLE_FIXTURE):
+        return {"error": "no oracle fixture (tests/golden/make_bench_oracle.py)"}
+    import hashlib
+    with np.load(ORACLE_FIXTURE, allow_pickle=False) as z:
+        fx = {k: z[k] for k in z.files}
+    h = hashlib.sha256()
+    for t in tracks:
+        h.update(np.ascontiguousarray(t, np.float32).tobytes())
+    if int(fx["frames"]) != frames or str(fx["corpus_sha256"]) != h.hexdigest() or \
+            not np.array_equal(fx["pairs"], pairs):
+        return {"error": "oracle fixture is for another corpus/length"}
+    q = fx["qmax"]
+    gq = Dfull[pairs[:, 0], pairs[:, 1]].astype(np.float32)
+    Do = np.zeros_like(Dfull)
+    Do[pairs[:, 0], pairs[:, 1]] = q
+    Dos = (Do + Do.T).astype(np.float32)
+    Dos = (Dos / np.sqrt(lens.astype(np.float64))[None, :]).astype(np.float32)
+    oMR, oMRR, oMDR, oMAP, otops = evaluation.eval_statistics(Dos, labels)
+    MR, MRR, MDR, MAP, tops = gpu_stats
+    st = lambda a, b, c, d, e: {"MAP": float(d), "MR1": float(a), "MRR": float(b), "MDR": float(c),  # noqa: E731
+                                "top": [int(t) for t in e]}
+    same = bool(np.array_equal(Dos, Dsym) and MAP == oMAP and MR == oMR and MRR == oMRR and MDR == oMDR
+                and np.array_equal(tops, otops))
+    return {"pairs_compared": int(len(q)), "qmax_pairs_differing": int(np.sum(gq != q)),
+            "gpu": st(MR, MRR, MDR, MAP, tops), "oracle": st(oMR, oMRR, oMDR, oMAP, otops),
+            "ds_bitexact": bool(np.array_equal(Dos, Dsym)), "identical": same,
+            "oracle_source": "tests/golden/bench_oracle_qmax.npz (oracle/crp_oracle.cpp, every pair)"}
+
+
 def host_info():
     model = None
     try:
@@ -129,10 +178,11 @@ def main():
     ap.add_argument("--frames", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=20250101)
     ap.add_argument("--corpus", choices=["hard", "bench"], default="hard")
-    ap.add_argument("--cpu-sample", type=int, default=-1,
-                    help="pairs timed on the CPU baseline: -1 = the whole step (every pair, at N=1: it also gives "
-                         "the oracle-side MAP/MR1), 0 = skip, k = k random pairs")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on")
+    ap.add_argument("--cpu-sample", type=int, default=320,
+                    help="pairs timed on the CPU baseline (~25 s on 16 threads at 2000 frames): 0 = skip, "
+                         "-1 = the whole step")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the box's CPU share (OMP_NUM_THREADS, else every CPU this process may run on)")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
 
@@ -274,43 +324,30 @@ def main():
                     "valu_issue": valu}
 
         map_parity, cpu = None, None
+        if world == 1 and args.corpus == "hard":
+            map_parity = oracle_map_parity(tracks, labels, lens, my_pairs_np, Dfull, Dsym, args.frames,
+                                           (MR, MRR, MDR, MAP, tops))
         if args.cpu_sample != 0:
             import oracle
             from acoss.synthetic import pack
             feats, off, ln = pack(tracks)
-            nth = args.cpu_threads or len(os.sched_getaffinity(0))
-            if args.cpu_sample < 0 and world == 1:
-                sp = my_pairs_np
-                what = "the whole step: all %d pairs of the corpus" % len(sp)
-            else:
-                rng = np.random.Generator(np.random.PCG64(1234))
-                k = len(my_pairs_np) if args.cpu_sample < 0 else min(args.cpu_sample, len(my_pairs_np))
-                k = min(k, 640) if world > 1 else k
-                sp = my_pairs_np[rng.choice(len(my_pairs_np), size=k, replace=False)]
-                what = "%d random pairs of the same corpus" % len(sp)
+            nth = args.cpu_threads or cpu_share()
+            rng = np.random.Generator(np.random.PCG64(1234))
+            k = min(args.cpu_sample if args.cpu_sample > 0 else len(my_pairs_np), len(my_pairs_np))
+            sp = my_pairs_np[np.sort(rng.choice(len(my_pairs_np), size=k, replace=False))]
+            what = ("the whole step: all %d pairs" % k) if k == len(my_pairs_np) else \
+                   ("%d random pairs of the step's %d" % (k, len(my_pairs_np)))
             log("cpu baseline: %s on %d threads" % (what, nth))
             t0 = time.perf_counter()
             q, _, _ = oracle.crp_batch(feats, off, ln, sp, dmax=False, nthreads=nth)
             cdt = time.perf_counter() - t0
             gq = Dfull[sp[:, 0], sp[:, 1]]
             cpu = {"value": round(len(sp) / cdt, 3), "unit": "song-pairs/s", "cores": nth, "kind": "port",
-                   "sample": "%s (%dx%d frames), oracle/crp_oracle.cpp, %d OpenMP threads, %.1f s"
-                             % (what, args.frames, args.frames, nth, cdt),
+                   "sample": "%s (%dx%d frames), oracle/crp_oracle.cpp, %d OpenMP threads (the box's CPU share), "
+                             "%.1f s" % (what, args.frames, args.frames, nth, cdt),
                    "host": host_info(),
                    "qmax_bitexact_vs_gpu": bool(np.array_equal(gq.astype(np.float32), q)),
                    "qmax_pairs_differing": int(np.sum(gq.astype(np.float32) != q))}
-            if len(sp) == total_pairs:  # the oracle scored every pair: MAP/MR1 on its own matrix
-                Do = np.zeros_like(Dfull)
-                Do[sp[:, 0], sp[:, 1]] = q
-                Dos = (Do + Do.T).astype(np.float32)
-                Dos = (Dos / np.sqrt(lens.astype(np.float64))[None, :]).astype(np.float32)
-                oMR, oMRR, oMDR, oMAP, otops = evaluation.eval_statistics(Dos, labels)
-                map_parity = {"gpu": {"MAP": float(MAP), "MR1": float(MR), "MRR": float(MRR), "MDR": float(MDR),
-                                      "top": [int(t) for t in tops]},
-                              "oracle": {"MAP": float(oMAP), "MR1": float(oMR), "MRR": float(oMRR),
-                                         "MDR": float(oMDR), "top": [int(t) for t in otops]},
-                              "ds_bitexact": bool(np.array_equal(Dos, Dsym)),
-                              "identical": bool(np.array_equal(Dos, Dsym) and MAP == oMAP and MR == oMR)}
 
         result = {
             "metric": "song-pairs/sec (CSM+Qmax) on 12-d HPCP, ~2000 frames/track; MAP parity",

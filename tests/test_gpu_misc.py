@@ -230,3 +230,32 @@ def test_simple_max_length_vs_oracle(lib):
         k = oracle.simple_oti(feats[i], feats[j])
         assert oti[p] == k
         assert score[p] == oracle.simple_sim(feats[i], feats[j], 10, k=k), (i, j)
+
+
+@pytest.mark.parametrize("env", [
+    {"ACOSS_SIMPLE_SH": "0"},                                        # K = 4 without frame passing
+    {"ACOSS_SIMPLE_PPB": "2"},                                       # 2 pairs per block
+    {"ACOSS_SIMPLE_K": "4", "ACOSS_SIMPLE_SH": "0", "ACOSS_SIMPLE_PPB": "2", "ACOSS_SIMPLE_RED": "1"},
+    {"ACOSS_SIMPLE_K": "2", "ACOSS_SIMPLE_RED": "1"},                # LDS row-minimum chunks
+    {"ACOSS_SIMPLE_K": "0"},                                         # invalid overrides fall back to the default
+    {"ACOSS_SIMPLE_K": "junk", "ACOSS_SIMPLE_PPB": "3"},
+])
+def test_simple_kernel_variants_vs_oracle(lib, monkeypatch, env):
+    """Every SiMPle kernel variant reachable through the overrides, on short ragged tracks, bit-exact;
+    the pairs name only some of the tracks (per-track scratch is built for those alone)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(17)
+    feats = []
+    for n in [40, 12, 150, 199, 10, 77, 130, 64]:
+        F = np.abs(rng.standard_normal((12, n)))
+        F /= np.linalg.norm(F, axis=0, keepdims=True)
+        feats.append(F)
+    used = [0, 2, 3, 5, 6]
+    pairs = np.array([(i, j) for i in used for j in used], dtype=np.int32)
+    score, oti = lib.simple_mp(feats, pairs)
+    score, oti = _np(score), _np(oti)
+    for p, (i, j) in enumerate(pairs):
+        k = oracle.simple_oti(feats[i], feats[j])
+        assert oti[p] == k
+        assert score[p] == oracle.simple_sim(feats[i], feats[j], 10, k=k), (i, j, env)

@@ -147,3 +147,23 @@ def test_eval_ranks_ties_inf_nan():
     sg = evaluation.eval_statistics_device(torch.as_tensor(D).cuda(), cliques=cliques)
     for a, b in zip(sg[:4], so[:4]):
         assert (a == b) or (np.isnan(a) and np.isnan(b)), (a, b)
+
+
+@pytest.mark.parametrize("slots", ["0", "1", "4", "32", "128"])
+def test_hr_ring_slots(monkeypatch, slots):
+    """The row-major key plane as per-XCD rings of strip slots (ACOSS_HR_RING; 1 slot per XCD
+    serialises the sweep blocks of each XCD through one buffer) against the oracle, including
+    short (LineS) and long (Line2) lines in one launch."""
+    from acoss.engine import ChromaBank
+    monkeypatch.setenv("ACOSS_HR_RING", slots)
+    rng = np.random.default_rng(int(slots) + 3)
+    lens = list(rng.integers(60, 1300, size=9)) + [2300, 480]
+    tracks = [synthetic.render(rng, synthetic.base_sequence(rng, int(n))) for n in lens]
+    pairs = _all_pairs(len(tracks))
+    feats, off, ln = synthetic.pack(tracks)
+    oq, od, _ = oracle.crp_batch(feats, off, ln, pairs, dmax=True, nthreads=_threads())
+    bank = ChromaBank(tracks)
+    for _ in range(2):  # a second call reuses the rings (tickets keep counting)
+        out = bank.crp_align(pairs, qmax=True, dmax=True)
+        np.testing.assert_array_equal(out["qmax"].cpu().numpy(), oq)
+        np.testing.assert_array_equal(out["dmax"].cpu().numpy(), od)

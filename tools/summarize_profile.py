@@ -1,12 +1,15 @@
 """Summarise a profiles/profile.sh run (gpurun_out/prof_<tag>) into profiles/<round>/.
 
-    python tools/summarize_profile.py <tag> <round_dir> [calls]
+    python tools/summarize_profile.py <tag> <round_dir> [calls] [corpus] [frames]
 
 Writes <round_dir>/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats), <tag>_pmc.json
-(SQ counters and HBM bytes per kernel) and profiles/traffic_latest.json (HBM bytes per
-acoss_crp_align call, for bench.py's roofline.traffic). HBM bytes follow MI355X_MICROARCH.md
-§HBM: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads half of a wide
-streaming read, so it is doubled.
+(SQ counters and HBM bytes per kernel), profiles/traffic_latest.json (HBM bytes per
+acoss_crp_align call, bench.py's roofline.traffic) and profiles/valu_latest.json (per kernel:
+average duration from the kernel trace, VALU wave-instructions per launch, and the VALU-issue
+fraction = SQ_INSTS_VALU / (duration x 614.4 G wave-instructions/s: 256 CUs x 4 SIMDs x 2.4 GHz /
+4 cycles per wave64 instruction), bench.py's roofline.valu_issue). HBM bytes follow
+MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads half
+of a wide streaming read, so it is doubled (the counters include Infinity-Cache hits).
 """
 import collections
 import csv
@@ -17,6 +20,9 @@ import sys
 
 tag, rdir = sys.argv[1], sys.argv[2]
 calls = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+corpus = sys.argv[4] if len(sys.argv) > 4 else "hard"
+frames = int(sys.argv[5]) if len(sys.argv) > 5 else 2000
+PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
 src = os.path.join("gpurun_out", "prof_" + tag)
 os.makedirs(rdir, exist_ok=True)
 shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(rdir, tag + "_kernel_stats.csv"))
@@ -37,10 +43,35 @@ for k, v in out.items():
     v["hbm_bytes_corrected"] = hbm
     tot += hbm
 json.dump(out, open(os.path.join(rdir, tag + "_pmc.json"), "w"), indent=1, sort_keys=True)
-json.dump({"source": os.path.join(rdir, tag + "_pmc.json"), "calls": calls, "frames": 2000,  # profile.sh: bench defaults
+json.dump({"source": os.path.join(rdir, tag + "_pmc.json"), "calls": calls, "frames": frames, "corpus": corpus,
            "hbm_bytes_per_launch": tot / calls,
            "note": "sum over all acoss kernels of 1024*(2*FETCH_SIZE+WRITE_SIZE) / acoss_crp_align calls"},
           open(os.path.join("profiles", "traffic_latest.json"), "w"), indent=1)
+# per-kernel durations (kernel trace, one stream) and VALU-issue fractions
+dur = {}
+for r in csv.DictReader(open(os.path.join(src, "kt", "run_kernel_stats.csv"))):
+    name = r["Name"]
+    if "acoss" not in name:
+        continue
+    k = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("acoss::", "")
+    dur[k] = {"calls": int(r["Calls"]), "total_ms": float(r["TotalDurationNs"]) / 1e6,
+              "avg_ms": float(r["AverageNs"]) / 1e6}
+valu = {}
+for k, d in dur.items():
+    v = out.get(k, {})
+    instr = v.get("SQ_INSTS_VALU", 0.0)
+    valu[k] = dict(d, valu_instr_per_call=instr / calls, hbm_bytes_per_call=v.get("hbm_bytes_corrected", 0.0) / calls,
+                   valu_issue_frac=(instr / (d["total_ms"] * 1e-3 * PEAK_WAVE_INSTR)) if d["total_ms"] > 0 else None)
+ksum = sum(d["total_ms"] for d in dur.values()) / calls
+json.dump({"source": os.path.join(rdir, tag + "_kernel_stats.csv") + " + " + os.path.join(rdir, tag + "_pmc.json"),
+           "calls": calls, "frames": frames, "corpus": corpus, "streams": 1,
+           "kernel_ms_per_call": ksum, "kernels": valu,
+           "peak_wave_instr_per_s": PEAK_WAVE_INSTR},
+          open(os.path.join("profiles", "valu_latest.json"), "w"), indent=1)
+print("kernel ms per call (one stream): %.3f" % ksum)
+for k, v in sorted(valu.items(), key=lambda kv: -kv[1]["total_ms"]):
+    print("  %-32s %9.3f ms/call  valu issue %s" % (k[:32], v["total_ms"] / calls,
+                                                    "%.3f" % v["valu_issue_frac"] if v["valu_issue_frac"] else "-"))
 print("HBM bytes per call: %.3e" % (tot / calls))
 for k, v in sorted(out.items()):
     print("%-40s hbm=%.3e  valu=%.3e" % (k[:40], v["hbm_bytes_corrected"], v.get("SQ_INSTS_VALU", 0)))
