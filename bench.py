@@ -119,6 +119,115 @@ def oracle_map_parity(tracks, labels, lens, pairs, Dfull, Dsym, frames, gpu_stat
             "oracle_source": "tests/golden/bench_oracle_qmax.npz (oracle/crp_oracle.cpp, every pair)"}
 
 
+PEAK_F64_TFLOPS = 78.6  # MI355X fp64 vector dense peak, MI355X_MICROARCH.md
+
+
+def other_paths(nth, seed):
+    """The other scorers on the path on one GPU, each timed with HIP events
+    on its launch stream beside a CPU oracle sample of the same inputs:
+      simple: SiMPle (Simple.oti + matrix profile + median, simple_silva.py:45-126) on every ORDERED
+        pair of 164 tracks x 2000 columns of unit-column float64 features (the covers80-shaped hard
+        corpus as SiMPle features); ops/pair = 2*12*na*nb + 16*(na-9)*(nb-9), f64 VALU.
+      earlyfusion: EarlyFusion.similarity (earlyfusion_traile.py:157-198) batched over every pair of
+        80 tracks x 446 beat blocks (synthetic block features); flops/pair = 2*(1000+1225+480)*M*N
+        on the fp32 MFMA CSMs, plus 4 SW and 3 WCSMs.
+    """
+    import torch
+    import oracle
+    from acoss import _lib, synthetic
+    from oracle import np_oracle as npo
+    res = {}
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # ---- SiMPle
+    tracks, _ = synthetic.make_hard_corpus("covers80", frames=2000, seed=seed)
+    feats = []
+    for t in tracks:
+        F = np.ascontiguousarray(np.asarray(t, np.float64).T) + 1e-3
+        feats.append(F / np.linalg.norm(F, axis=0, keepdims=True))
+    T = len(feats)
+    n = feats[0].shape[1]
+    flat = np.concatenate([f.ravel() for f in feats])
+    off = np.arange(T, dtype=np.int64) * 12 * n
+    lens = np.full(T, n, np.int32)
+    pairs = np.array([(i, j) for i in range(T) for j in range(T) if i != j], np.int32)
+    flat_d, pt = torch.as_tensor(flat).cuda(), torch.as_tensor(pairs).cuda()
+    _lib.simple_mp_packed(flat_d, off, lens, pt)
+    torch.cuda.synchronize()
+    ev0.record()
+    score, _ = _lib.simple_mp_packed(flat_d, off, lens, pt)
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1)
+    ops = 2.0 * 12 * n * n + 16.0 * (n - 9) * (n - 9)
+    sp = pairs[np.random.Generator(np.random.PCG64(3)).choice(len(pairs), 960, replace=False)]
+    t0 = time.perf_counter()
+    cs, _ = oracle.simple_batch(flat, off, lens, sp, nthreads=nth)
+    cdt = time.perf_counter() - t0
+    g = score.cpu().numpy()
+    idx = sp[:, 0] * (T - 1) + sp[:, 1] - (sp[:, 1] > sp[:, 0])
+    res["simple"] = {"metric": "ordered song-pairs/s (SiMPle matrix profile, 2000 columns)",
+                     "value": round(len(pairs) / (ms * 1e-3), 1), "ms": round(ms, 3), "pairs": int(len(pairs)),
+                     "dtype": "f64",
+                     "roofline": {"bound": "valu", "achieved": round(ops * len(pairs) / (ms * 1e-3) / 1e12, 3),
+                                  "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": round(ops * len(pairs) / (ms * 1e-3) / 1e12 / PEAK_F64_TFLOPS, 4),
+                                  "ops_per_pair": ops},
+                     "cpu_baseline": {"value": round(len(sp) / cdt, 3), "cores": nth, "kind": "port",
+                                      "sample": "%d ordered pairs, oracle or_simple_batch, %.1f s" % (len(sp), cdt)},
+                     "bitexact_vs_oracle": bool(np.array_equal(g[idx], cs))}
+    # ---- EarlyFusion
+    rng = np.random.Generator(np.random.PCG64(seed))
+    NT, NB = 80, 446
+    mf = rng.standard_normal((NT * NB, 1000), dtype=np.float32)
+    ss = np.abs(rng.standard_normal((NT * NB, 1225), dtype=np.float32))
+    ch = np.abs(rng.standard_normal((NT * NB, 480), dtype=np.float32))
+    med = np.abs(rng.standard_normal((NT, 12), dtype=np.float32))
+    bank = {"mfccs": torch.as_tensor(mf).cuda(), "ssms": torch.as_tensor(ss).cuda(), "chromas": torch.as_tensor(ch).cuda(),
+            "chroma_med": torch.as_tensor(med).cuda(),
+            "off": torch.as_tensor(np.arange(NT, dtype=np.int64) * NB).cuda(),
+            "nb": torch.as_tensor(np.full(NT, NB, np.int32)).cuda(), "max_blocks": NB}
+    epairs = np.array([(i, j) for i in range(NT) for j in range(i + 1, NT)], np.int32)
+    _lib.earlyfusion(bank, epairs[:64], 0.1, 10)
+    torch.cuda.synchronize()
+    ev0.record()
+    esc = _lib.earlyfusion(bank, epairs, 0.1, 10)
+    ev1.record()
+    torch.cuda.synchronize()
+    ems = ev0.elapsed_time(ev1)
+    flops = 2.0 * (1000 + 1225 + 480) * NB * NB
+    esc = esc.cpu().numpy().reshape(-1, 4)
+    t0 = time.perf_counter()
+    agree = 0
+    ncpu = 24
+    for p in range(ncpu):
+        i, j = epairs[p * 97 % len(epairs)]
+        f1 = {"mfccs": mf[i * NB:(i + 1) * NB], "ssms": ss[i * NB:(i + 1) * NB], "chromas": ch[i * NB:(i + 1) * NB],
+              "chroma_med": med[i]}
+        f2 = {"mfccs": mf[j * NB:(j + 1) * NB], "ssms": ss[j * NB:(j + 1) * NB], "chromas": ch[j * NB:(j + 1) * NB],
+              "chroma_med": med[j]}
+        C = [npo.get_csm(f1["mfccs"], f2["mfccs"]), npo.get_csm(f1["ssms"], f2["ssms"]),
+             npo.get_csm_blocked_oti(f1["chromas"], f2["chromas"], f1["chroma_med"], f2["chroma_med"],
+                                     npo.get_csm_cosine)]
+        W = np.zeros_like(C[0])
+        for c in C:
+            W += npo.getWCSM(c, 10, 10)
+        ref = [oracle.sw_constrained(npo.csm_to_binary(M, 0.1)) for M in C + [np.exp(-W)]]
+        agree += int(np.sum(np.asarray(ref) == esc[p * 97 % len(epairs)]))
+    cdt = time.perf_counter() - t0
+    res["earlyfusion"] = {"metric": "song-pairs/s (EarlyFusion: 3 CSMs + kNN + WCSM fusion + 4 SW, 446 blocks)",
+                          "value": round(len(epairs) / (ems * 1e-3), 1), "ms": round(ems, 3),
+                          "pairs": int(len(epairs)), "dtype": "f32",
+                          "roofline": {"bound": "mfma",
+                                       "achieved": round(flops * len(epairs) / (ems * 1e-3) / 1e12, 3),
+                                       "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                                       "frac": round(flops * len(epairs) / (ems * 1e-3) / 1e12 / PEAK_F32_TFLOPS, 4),
+                                       "flops_per_pair": flops},
+                          "cpu_baseline": {"value": round(ncpu / cdt, 3), "cores": 1, "kind": "port",
+                                           "sample": "%d pairs, numpy restatement + C SW oracle, %.1f s" % (ncpu, cdt)},
+                          "scores_equal_to_oracle": "%d of %d" % (agree, 4 * ncpu)}
+    return res
+
+
 def host_info():
     model = None
     try:
@@ -178,12 +287,13 @@ def main():
     ap.add_argument("--frames", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=20250101)
     ap.add_argument("--corpus", choices=["hard", "bench"], default="hard")
-    ap.add_argument("--cpu-sample", type=int, default=320,
-                    help="pairs timed on the CPU baseline (~25 s on 16 threads at 2000 frames): 0 = skip, "
-                         "-1 = the whole step")
+    ap.add_argument("--cpu-sample", type=int, default=4000,
+                    help="pairs timed on the CPU baseline (~15 s on the box's 16 threads at 2000 frames): "
+                         "0 = skip, -1 = the whole step")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = the box's CPU share (OMP_NUM_THREADS, else every CPU this process may run on)")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-paths", action="store_true", help="skip the SiMPle / EarlyFusion lines")
     args = ap.parse_args()
 
     import torch
@@ -349,6 +459,11 @@ def main():
                    "qmax_bitexact_vs_gpu": bool(np.array_equal(gq.astype(np.float32), q)),
                    "qmax_pairs_differing": int(np.sum(gq.astype(np.float32) != q))}
 
+        paths = None
+        if world == 1 and not args.no_paths:
+            log("other paths (SiMPle, EarlyFusion)")
+            paths = other_paths(args.cpu_threads or cpu_share(), args.seed)
+
         result = {
             "metric": "song-pairs/sec (CSM+Qmax) on 12-d HPCP, ~2000 frames/track; MAP parity",
             "value": round(value, 2), "unit": "song-pairs/s", "n_gpus": n_gpus, "steps": args.steps,
@@ -363,6 +478,7 @@ def main():
             "top1": int(tops[0]), "map_parity": map_parity,
             "roofline": roofline, "cpu_baseline": cpu,
             "speedup_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
+            "other_paths": paths,
         }
         print(json.dumps(result))
     if world > 1:

@@ -61,6 +61,8 @@ def lib():
         L.or_oti.argtypes = [_fp, _fp]
         L.or_simple_oti.restype = ctypes.c_int
         L.or_simple_oti.argtypes = [_dp, ctypes.c_int, _dp, ctypes.c_int]
+        L.or_simple_batch.restype = ctypes.c_int
+        L.or_simple_batch.argtypes = [_dp, _i64p, _i32p, _i32p, ctypes.c_int64, ctypes.c_int, _dp, _i32p, ctypes.c_int]
         L.or_ess_compare_batch.restype = ctypes.c_int
         L.or_ess_compare_batch.argtypes = [_fp, _i64p, _i32p, _i32p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -191,6 +193,20 @@ def simple_sim(A, B, sslen=10, k=0):
     A = np.ascontiguousarray(A, np.float64)
     B = np.ascontiguousarray(B, np.float64)
     return float(lib().or_simple_sim(_p(A, _dp), A.shape[1], _p(B, _dp), B.shape[1], int(k), sslen))
+
+
+def simple_batch(flat, off, lens, pairs, sslen=10, nthreads=0):
+    """Simple.oti + simple_sim for ordered pairs of packed (12 x n) float64 blocks (element
+    offsets `off`, columns `lens`): (score (P,) float64, oti (P,) int32)."""
+    flat = np.ascontiguousarray(flat, np.float64)
+    off = np.ascontiguousarray(off, np.int64)
+    lens = np.ascontiguousarray(lens, np.int32)
+    pairs = np.ascontiguousarray(pairs, np.int32)
+    P = len(pairs)
+    score, k = np.zeros(P), np.zeros(P, np.int32)
+    lib().or_simple_batch(_p(flat, _dp), _p(off, _i64p), _p(lens, _i32p), _p(pairs, _i32p), P, int(sslen),
+                          _p(score, _dp), _p(k, _i32p), int(nthreads))
+    return score, k
 
 
 def profile(X):

@@ -596,4 +596,21 @@ int or_simple_oti(const double* A, int na, const double* B, int nb) {
   return best;
 }
 
+// SiMPle over a batch of ordered pairs of packed (12 x n_t) float64 blocks (element offsets),
+// with the Simple.oti roll: the CPU baseline of bench.py's SiMPle line. OpenMP over pairs.
+int or_simple_batch(const double* feats, const int64_t* off, const int32_t* len, const int32_t* pairs,
+                    int64_t n_pairs, int L, double* score, int32_t* oti, int nthreads) {
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int64_t p = 0; p < n_pairs; ++p) {
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    const int k = or_simple_oti(feats + off[a], len[a], feats + off[b], len[b]);
+    if (oti) oti[p] = k;
+    score[p] = or_simple_sim(feats + off[a], len[a], feats + off[b], len[b], k, L);
+  }
+  return 0;
+}
+
 }  // extern "C"
