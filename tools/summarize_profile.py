@@ -23,6 +23,9 @@ calls = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 corpus = sys.argv[4] if len(sys.argv) > 4 else "hard"
 frames = int(sys.argv[5]) if len(sys.argv) > 5 else 2000
 PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
+# the kernels acoss_crp_align launches (prep, OTI, roll, sweep + row select, column select, DP)
+CRP_KERNEL = lambda n: any(s in n for s in ("k_track_", "k_pair_oti", "k_rotate_ref", "k_sweep_rows9", "k_sel_cols9",
+                                            "k_crp_"))  # noqa: E731
 src = os.path.join("gpurun_out", "prof_" + tag)
 os.makedirs(rdir, exist_ok=True)
 shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(rdir, tag + "_kernel_stats.csv"))
@@ -33,7 +36,7 @@ for part in ("sq", "fetch", "write"):
         continue
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        if "acoss" not in name:
+        if "acoss" not in name or not CRP_KERNEL(name):
             continue
         k = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("acoss::", "")
         out[k][r["Counter_Name"]] = out[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -51,7 +54,7 @@ json.dump({"source": os.path.join(rdir, tag + "_pmc.json"), "calls": calls, "fra
 dur = {}
 for r in csv.DictReader(open(os.path.join(src, "kt", "run_kernel_stats.csv"))):
     name = r["Name"]
-    if "acoss" not in name:
+    if "acoss" not in name or not CRP_KERNEL(name):
         continue
     k = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("acoss::", "")
     dur[k] = {"calls": int(r["Calls"]), "total_ms": float(r["TotalDurationNs"]) / 1e6,
