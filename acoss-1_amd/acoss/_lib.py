@@ -50,6 +50,8 @@ SIGNATURES = {
     "acoss_simple_features": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _i64, _vp],
     "acoss_earlyfusion": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, ctypes.c_double,
                           _i32, _f32, _vp, _vp],
+    "acoss_ef_block_features": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp,
+                                _vp, _vp],
     "acoss_ds_finish": [_vp, _i32, _i64, _vp, _i32, _i32, _vp, _vp],
     "acoss_eval_ranks": [_vp, _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp],
     "acoss_release_workspace": [],
@@ -452,6 +454,61 @@ def earlyfusion(bank, pairs, kappa=0.1, K=10, mu=0.5):
                                int(bank["mfccs"].shape[1]), int(bank["ssms"].shape[1]), int(bank["chromas"].shape[1]),
                                _ptr(pairs), int(P), float(kappa), int(K), float(mu), _ptr(out), _stream())
     _check(rc, "acoss_earlyfusion")
+    return out
+
+
+def ef_block_features(chromas, mfccs, onsets, blocksize=20, mfccs_per_block=50, chromas_per_block=40):
+    """EarlyFusion block features of a batch of tracks on the device (acoss_ef_block_features).
+    chromas: list of (n_t, 12); mfccs: list of (n_t, d) frame-major (mfcc_htk.T); onsets: list of
+    frame-index arrays. NaN MFCCs become 0 (earlyfusion_traile.py:98). Returns a dict of device
+    tensors 'mfccs' (B, R*d), 'ssms' (B, R(R-1)/2), 'chromas' (B, Rc*12), 'chroma_med' (T, 12)
+    and host 'block_off' (T,) int64 / 'n_blocks' (T,) int32 (blocks of track t: rows
+    block_off[t] .. + n_blocks[t])."""
+    torch = _torch()
+    lib = load_library()
+    T = len(chromas)
+    if not (len(mfccs) == len(onsets) == T):
+        raise ValueError("one chroma, mfcc and onset array per track")
+    n = np.array([len(c) for c in chromas], np.int64)
+    d = int(np.asarray(mfccs[0]).shape[1]) if T else 20
+    nb = np.zeros(T, np.int64)
+    for t in range(T):
+        o = np.asarray(onsets[t], np.int64)
+        if np.asarray(mfccs[t]).shape != (n[t], d):
+            raise ValueError("track %d: mfcc must be (n_frames, %d) like its chroma" % (t, d))
+        nb[t] = max(0, len(o) - blocksize)
+        if nb[t]:
+            if o.min() < 0 or o.max() > n[t] or np.any(np.diff(o) <= 0):
+                raise ValueError("track %d: onsets must increase inside the track" % t)
+            span = o[blocksize:] - o[:-blocksize]
+            if span.max() > 256 * min(mfccs_per_block, chromas_per_block):
+                raise ValueError("track %d: a beat block spans more than %d frames" %
+                                 (t, 256 * min(mfccs_per_block, chromas_per_block)))
+    foff = np.zeros(T, np.int64)
+    foff[1:] = np.cumsum(n[:-1])
+    ooff = np.zeros(T, np.int64)
+    ooff[1:] = np.cumsum([len(o) for o in onsets][:-1])
+    boff = np.zeros(T, np.int64)
+    boff[1:] = np.cumsum(nb[:-1])
+    B = int(nb.sum())
+    mf = np.concatenate([np.asarray(m, np.float32) for m in mfccs]) if T else np.zeros((0, d), np.float32)
+    mf = np.where(np.isnan(mf), np.float32(0), mf)
+    ch = np.concatenate([np.asarray(c, np.float32) for c in chromas]) if T else np.zeros((0, 12), np.float32)
+    on = np.concatenate([np.asarray(o, np.int64) for o in onsets]) if T else np.zeros(0, np.int64)
+    d_mf, d_ch = _dev(mf, torch.float32), _dev(ch, torch.float32)
+    d_foff, d_n = _dev(foff, torch.int64), _dev(n.astype(np.int32), torch.int32)
+    d_on, d_ooff, d_boff = _dev(on, torch.int64), _dev(ooff, torch.int64), _dev(boff, torch.int64)
+    R, Rc = int(mfccs_per_block), int(chromas_per_block)
+    out = {"mfccs": torch.empty((B, R * d), dtype=torch.float32, device="cuda"),
+           "ssms": torch.empty((B, R * (R - 1) // 2), dtype=torch.float32, device="cuda"),
+           "chromas": torch.empty((B, Rc * 12), dtype=torch.float32, device="cuda"),
+           "chroma_med": torch.empty((T, 12), dtype=torch.float32, device="cuda")}
+    rc = lib.acoss_ef_block_features(_ptr(d_mf), _ptr(d_ch), _ptr(d_foff), _ptr(d_n), _ptr(d_on), _ptr(d_ooff),
+                                     _ptr(d_boff), T, B, int(blocksize), R, Rc, d, _ptr(out["mfccs"]),
+                                     _ptr(out["ssms"]), _ptr(out["chromas"]), _ptr(out["chroma_med"]), _stream())
+    _check(rc, "acoss_ef_block_features")
+    out["block_off"] = boff
+    out["n_blocks"] = nb.astype(np.int32)
     return out
 
 

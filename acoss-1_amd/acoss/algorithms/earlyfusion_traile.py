@@ -8,11 +8,14 @@ Per pair (A15, :157-198) everything runs on the GPU through the C-ABI: three CSM
 blocks), kappa-NN binarisation, getWCSM of each CSM, their sum -> exp(-sum) -> binarisation,
 and the four constrained Smith-Waterman alignments of a chunk in one launch.
 
-The beat-synchronous block features (load_features, :67-154) are per-track preprocessing
- and run on the host. They need skimage.transform.resize, which this
-image lacks: `resize_block` restates skimage >= 0.19 `resize(..., anti_aliasing=True,
-mode='constant')` (Gaussian pre-filter with sigma = max(0, (factor - 1) / 2), then a
-grid-mode linear zoom with zero fill) with scipy.ndimage. That restatement is unpinned.
+The beat-synchronous block features (load_features, :67-154) are computed
+on the GPU too (efblocks.hip acoss_ef_block_features: every block of a batch of tracks in one
+launch, skimage's resize restated in float64), batched over all songs in prepare() and cached on
+disk as the reference does. `resize_block` (:214-247) stays as the reference's public helper: it
+restates skimage >= 0.19 `resize(..., anti_aliasing=True, mode='constant')` (Gaussian pre-filter
+with sigma = max(0, (factor - 1) / 2), then a grid-mode linear zoom with zero fill) with
+scipy.ndimage. skimage is absent here, so both restatements are pinned against each other and
+against an independent loop restatement (tests/test_earlyfusion_host.py), not against skimage.
 """
 import argparse
 import os
@@ -48,14 +51,6 @@ def resize_block(X, i1, i2, frames_per_block, median_aggregate=False):
     return ret
 
 
-def _ssm_upper(xn, I, J):
-    sq = np.sum(xn ** 2, 1)
-    D = sq[:, None] + sq[None, :] - 2 * xn.dot(xn.T)
-    D[D < 0] = 0
-    np.fill_diagonal(D, 0)
-    return np.sqrt(D)[I < J]
-
-
 class EarlyFusion(CoverAlgorithm):
     def __init__(self, dataset_csv, datapath, chroma_type='hpcp', shortname='Covers80', blocksize=20,
                  mfccs_per_block=50, ssm_res=50, chromas_per_block=40, kappa=0.1, K=10, niters=5, log_times=False,
@@ -81,7 +76,7 @@ class EarlyFusion(CoverAlgorithm):
 
     def load_features(self, i, do_plot=False):
         """Blocked features of song i: 'mfccs', 'ssms', 'chromas', 'chroma_med' (:67-154),
-        cached in memory and on disk ('<prefix>_<i>.npz')."""
+        cached in memory and on disk ('<prefix>_<i>.npz'); computed on the GPU."""
         filepath = "%s_%i.h5" % (self.get_cacheprefix(), i)
         if i in self.all_block_feats:
             return self.all_block_feats[i]
@@ -91,37 +86,30 @@ class EarlyFusion(CoverAlgorithm):
             return self.all_block_feats[i]
         except IOError:
             pass
+        return self._compute_blocks([i])[0]
+
+    def _compute_blocks(self, idx):
+        """Block features of songs idx in one acoss_ef_block_features launch; cached in memory and
+        on disk like load_features."""
         tic = time.time()
-        feats = CoverAlgorithm.load_features(self, i)
-        chroma = np.asarray(feats[self.chroma_type])
-        mfcc = np.array(feats['mfcc_htk']).T
-        mfcc[np.isnan(mfcc)] = 0
-        onsets = np.asarray(feats['madmom_features']['onsets'])
-        n_blocks = len(onsets) - self.blocksize
-        bf = {}
-        bf['mfccs'] = np.zeros((n_blocks, self.mfccs_per_block * mfcc.shape[1]), dtype=np.float32)
-        pix = np.arange(self.mfccs_per_block)
-        I, J = np.meshgrid(pix, pix)
-        bf['ssms'] = np.zeros((n_blocks, int(self.mfccs_per_block * (self.mfccs_per_block - 1) / 2)),
-                              dtype=np.float32)
-        for b in range(n_blocks):
-            x = resize_block(mfcc, onsets[b], onsets[b + self.blocksize - 1], self.mfccs_per_block)
-            x -= np.mean(x, 0)[None, :]
-            xnorm = np.sqrt(np.sum(x ** 2, 1))[:, None]
-            xnorm[xnorm == 0] = 1
-            xn = x / xnorm
-            bf['mfccs'][b, :] = xn.flatten()
-            bf['ssms'][b, :] = _ssm_upper(xn, I, J)
-        bf['chromas'] = np.zeros((n_blocks, self.chromas_per_block * chroma.shape[1]), dtype=np.float32)
-        bf['chroma_med'] = np.median(chroma, axis=0)
-        for b in range(n_blocks):
-            x = resize_block(chroma, onsets[b], onsets[b + self.blocksize], self.chromas_per_block)
-            bf['chromas'][b, :] = x.flatten()
-        self.all_block_feats[i] = bf
-        _save_feature_file(filepath, bf)
+        feats = [CoverAlgorithm.load_features(self, i) for i in idx]
+        chroma = [np.asarray(f[self.chroma_type], np.float32) for f in feats]
+        mfcc = [np.array(f['mfcc_htk'], dtype=np.float32).T for f in feats]
+        onsets = [np.asarray(f['madmom_features']['onsets'], np.int64) for f in feats]
+        out = _lib.ef_block_features(chroma, mfcc, onsets, self.blocksize, self.mfccs_per_block,
+                                     self.chromas_per_block)
+        host = {k: out[k].cpu().numpy() for k in ("mfccs", "ssms", "chromas", "chroma_med")}
+        res = []
+        for t, i in enumerate(idx):
+            b0, nb = int(out["block_off"][t]), int(out["n_blocks"][t])
+            bf = {"mfccs": host["mfccs"][b0:b0 + nb], "ssms": host["ssms"][b0:b0 + nb],
+                  "chromas": host["chromas"][b0:b0 + nb], "chroma_med": host["chroma_med"][t]}
+            self.all_block_feats[i] = bf
+            _save_feature_file("%s_%i.h5" % (self.get_cacheprefix(), i), bf)
+            res.append(bf)
         if self.log_times:
-            self.times['features'].append(time.time() - tic)
-        return bf
+            self.times['features'].append((time.time() - tic) / max(1, len(idx)))
+        return res
 
     def _device(self, i):
         if i not in self._dev:
@@ -183,10 +171,21 @@ class EarlyFusion(CoverAlgorithm):
         for s, key in enumerate(("mfccs", "ssms", "chromas", "early")):
             self.Ds[key][idxs[:, 0], idxs[:, 1]] = scores[:, s]
 
-    def prepare(self):
+    def prepare(self, chunk=256):
+        """Every song's block features: from the memory / disk cache, the rest on the GPU in
+        batches of `chunk` songs."""
         if not self._prepared:
+            missing = []
             for i in range(self.N):
-                self.load_features(i)
+                if i in self.all_block_feats:
+                    continue
+                try:
+                    self.all_block_feats[i] = _load_feature_file("%s_%i.h5" % (self.get_cacheprefix(), i))
+                    CoverAlgorithm.load_features(self, i)
+                except IOError:
+                    missing.append(i)
+            for c0 in range(0, len(missing), chunk):
+                self._compute_blocks(missing[c0:c0 + chunk])
             self._prepared = True
 
     def do_late_fusion(self):

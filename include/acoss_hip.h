@@ -173,6 +173,21 @@ int acoss_earlyfusion(const float* mfcc, const float* ssm, const float* chroma, 
                       int32_t d_mfcc, int32_t d_ssm, int32_t d_chroma, const int32_t* pairs, int64_t n_pairs,
                       double kappa, int32_t K, float mu, double* scores_out, void* hip_stream);
 
+/* EarlyFusion beat-synchronous block features of a batch of tracks (replaces
+ * EarlyFusion.load_features' block loops, acoss/algorithms/earlyfusion_traile.py:67-154, and its
+ * skimage resize_block, :214-247, restated in float64). Track t: frames [frame_off[t], +n_frames[t])
+ * of mfcc ((sum n) x d_mfcc, frame-major: mfcc_htk transposed, NaN already zeroed) and chroma
+ * ((sum n) x 12); onsets (frame indices, int64) at [onset_off[t], ...), its n_blocks = n_onsets -
+ * blocksize blocks at global block index block_off[t] .. (total_blocks in all). Outputs per global
+ * block: out_mfcc (mfccs_per_block * d_mfcc), out_ssm (mfccs_per_block (mfccs_per_block - 1) / 2),
+ * out_chroma (chromas_per_block * 12) float32; out_med (n_tracks x 12) = np.median(chroma, axis=0).
+ * Every block must span at least one frame and at most 256 * rows-per-block frames. */
+int acoss_ef_block_features(const float* mfcc, const float* chroma, const int64_t* frame_off, const int32_t* n_frames,
+                            const int64_t* onsets, const int64_t* onset_off, const int64_t* block_off,
+                            int32_t n_tracks, int64_t total_blocks, int32_t blocksize, int32_t mfccs_per_block,
+                            int32_t chromas_per_block, int32_t d_mfcc, float* out_mfcc, float* out_ssm,
+                            float* out_chroma, float* out_med, void* hip_stream);
+
 /* Finish of a pair-score matrix after the pair loop, in place when out == D.
  * D, out: (n x n) float32, row stride ld (elements). symmetric = 1 first forms D[i,j] + D[j,i] from
  * the original values (CoverAlgorithm.all_pairwise's `Ds += Ds.T`, algorithm_template.py:188-191);

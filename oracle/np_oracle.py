@@ -109,6 +109,47 @@ def simple_oti(seq_a, seq_b):
     return np.roll(seq_b, k, axis=0), k
 
 
+# acoss/algorithms/earlyfusion_traile.py:214-247 (resize_block, skimage.transform.resize restated:
+# skimage is absent, unpinned)
+def resize_block(X, i1, i2, frames_per_block):
+    from scipy import ndimage
+    x = np.asarray(X[i1:i2, :], dtype=np.float64)
+    factor = x.shape[0] / float(frames_per_block)
+    sigma = max(0.0, (factor - 1.0) / 2.0)
+    if sigma > 0:
+        x = ndimage.gaussian_filter(x, (sigma, 0.0), mode="constant", cval=0.0)
+    ret = ndimage.zoom(x, (frames_per_block / float(x.shape[0]), 1.0), order=1, mode="grid-constant", cval=0.0,
+                       grid_mode=True)
+    ret[np.isinf(ret)] = 0
+    ret[np.isnan(ret)] = 0
+    return ret
+
+
+# acoss/algorithms/earlyfusion_traile.py:100-150 (the block loops of EarlyFusion.load_features)
+def ef_block_features(chroma, mfcc_htk, onsets, blocksize=20, mfccs_per_block=50, chromas_per_block=40):
+    mfcc = np.array(mfcc_htk).T
+    mfcc[np.isnan(mfcc)] = 0
+    n_blocks = len(onsets) - blocksize
+    bf = {"mfccs": np.zeros((n_blocks, mfccs_per_block * mfcc.shape[1]), dtype=np.float32)}
+    pix = np.arange(mfccs_per_block)
+    I, J = np.meshgrid(pix, pix)
+    bf["ssms"] = np.zeros((n_blocks, int(mfccs_per_block * (mfccs_per_block - 1) / 2)), dtype=np.float32)
+    for b in range(n_blocks):
+        x = resize_block(mfcc, onsets[b], onsets[b + blocksize - 1], mfccs_per_block)
+        x -= np.mean(x, 0)[None, :]
+        xnorm = np.sqrt(np.sum(x ** 2, 1))[:, None]
+        xnorm[xnorm == 0] = 1
+        xn = x / xnorm
+        bf["mfccs"][b, :] = xn.flatten()
+        bf["ssms"][b, :] = get_ssm(xn)[I < J]
+    bf["chromas"] = np.zeros((n_blocks, chromas_per_block * chroma.shape[1]), dtype=np.float32)
+    bf["chroma_med"] = np.median(chroma, axis=0)
+    for b in range(n_blocks):
+        x = resize_block(chroma, onsets[b], onsets[b + blocksize], chromas_per_block)
+        bf["chromas"][b, :] = x.flatten()
+    return bf
+
+
 def snf_step(mats, skip, J, V, reg_diag):
     """One cross-diffusion step of doSimilarityFusionWs for matrix `skip`
     (acoss/algorithms/utils/similarity_fusion.py:163-174): the average of the other matrices,

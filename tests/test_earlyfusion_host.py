@@ -58,32 +58,34 @@ def test_resize_block_matches_direct_restatement(n_in, n_out):
     np.testing.assert_allclose(got, _resize_direct(X[10:10 + n_in], n_out), rtol=1e-12, atol=1e-12)
 
 
-def test_block_features_match_reference_loop(tmp_path):
-    """load_features' MFCC / SSM / chroma blocks vs the reference's loop (:107-126) built from
-    the pinned pieces: resize (restated above), z-normalisation, get_ssm upper triangle."""
-    from acoss import synthetic
-    from acoss.algorithms.earlyfusion_traile import EarlyFusion
+def test_oracle_block_features_match_reference_loop():
+    """np_oracle.ef_block_features (the checker of the GPU kernel acoss_ef_block_features) vs the
+    reference's loop (:107-126) built from the pinned pieces: resize (restated above),
+    z-normalisation, get_ssm upper triangle."""
     rng = np.random.default_rng(3)
-    tracks = [np.abs(rng.normal(size=(900, 12))).astype(np.float32)]
-    csv, fdir = synthetic.write_feature_dataset(str(tmp_path), tracks, np.array([0]), with_mfcc=True)
-    ef = EarlyFusion(csv, fdir, shortname="t", cachedir=str(tmp_path / "cache"))
-    bf = ef.load_features(0)
-    from acoss.features_io import load_features
-    raw = load_features(fdir + "W00000/T000000.h5")
-    mfcc = np.array(raw["mfcc_htk"]).T
-    onsets = raw["madmom_features"]["onsets"]
-    nb = len(onsets) - ef.blocksize
+    n = 900
+    chroma = np.abs(rng.normal(size=(n, 12))).astype(np.float32)
+    mfcc_htk = rng.normal(size=(20, n)).astype(np.float32)
+    mfcc_htk[3, 17] = np.nan  # NaN MFCCs become 0 (:98)
+    onsets = np.unique(np.clip(np.arange(0, n - 1, 43) + rng.integers(0, 3, size=len(range(0, n - 1, 43))), 0, n - 1))
+    bf = npo.ef_block_features(chroma, mfcc_htk, onsets)
+    mfcc = mfcc_htk.T.copy()
+    mfcc[np.isnan(mfcc)] = 0
+    nb = len(onsets) - 20
     assert bf["mfccs"].shape == (nb, 50 * 20) and bf["ssms"].shape == (nb, 1225) and bf["chromas"].shape == (nb, 480)
     pix = np.arange(50)
     I, J = np.meshgrid(pix, pix)
     for b in range(nb):
-        x = _resize_direct(mfcc[onsets[b]:onsets[b + ef.blocksize - 1]], 50)
+        x = _resize_direct(mfcc[onsets[b]:onsets[b + 19]], 50)
         x -= np.mean(x, 0)[None, :]
         xnorm = np.sqrt(np.sum(x ** 2, 1))[:, None]
         xnorm[xnorm == 0] = 1
         xn = x / xnorm
         np.testing.assert_allclose(bf["mfccs"][b], xn.flatten().astype(np.float32), rtol=2e-6, atol=1e-7)
         np.testing.assert_allclose(bf["ssms"][b], npo.get_ssm(xn)[I < J].astype(np.float32), rtol=2e-6, atol=2e-6)
-        c = _resize_direct(tracks[0][onsets[b]:onsets[b + ef.blocksize]], 40)
+        c = _resize_direct(chroma[onsets[b]:onsets[b + 20]], 40)
         np.testing.assert_allclose(bf["chromas"][b], c.flatten().astype(np.float32), rtol=2e-6, atol=1e-7)
-    np.testing.assert_array_equal(bf["chroma_med"], np.median(tracks[0], axis=0))
+    np.testing.assert_array_equal(bf["chroma_med"], np.median(chroma, axis=0))
+    # the product's public resize_block and the oracle's are the same restatement
+    from acoss.algorithms.earlyfusion_traile import resize_block
+    np.testing.assert_array_equal(resize_block(mfcc, 5, 300, 50), npo.resize_block(mfcc, 5, 300, 50))
