@@ -476,7 +476,10 @@ def ef_block_features(chromas, mfccs, onsets, blocksize=20, mfccs_per_block=50, 
         o = np.asarray(onsets[t], np.int64)
         if np.asarray(mfccs[t]).shape != (n[t], d):
             raise ValueError("track %d: mfcc must be (n_frames, %d) like its chroma" % (t, d))
-        nb[t] = max(0, len(o) - blocksize)
+        if len(o) < blocksize:  # the reference's np.zeros((n_beats - blocksize, ...)) raises here (:106)
+            raise ValueError("track %d: %d beats, fewer than blocksize=%d (negative dimensions are not allowed)"
+                             % (t, len(o), blocksize))
+        nb[t] = len(o) - blocksize
         if nb[t]:
             if o.min() < 0 or o.max() > n[t] or np.any(np.diff(o) <= 0):
                 raise ValueError("track %d: onsets must increase inside the track" % t)

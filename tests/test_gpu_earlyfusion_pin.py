@@ -160,7 +160,7 @@ def test_ef_block_features_gpu_vs_restatement():
     from acoss import _lib
     rng = np.random.default_rng(12)
     chromas, mfccs, onsets = [], [], []
-    for n, period in [(900, 43), (2601, 37), (500, 11), (4001, 60), (300, 90)]:
+    for n, period in [(900, 43), (2601, 37), (500, 11), (4001, 60), (860, 43)]:
         chromas.append(np.abs(rng.normal(size=(n, 12))).astype(np.float32))
         m = rng.normal(size=(20, n)).astype(np.float32)
         m[1, 5] = np.nan
@@ -181,3 +181,9 @@ def test_ef_block_features_gpu_vs_restatement():
             same += int(np.sum(got == ref[key]))
         np.testing.assert_array_equal(out["chroma_med"].cpu().numpy()[t], ref["chroma_med"])
     assert same >= 0.99 * tot, (same, tot)
+    # fewer beats than blocksize: the reference raises (np.zeros with a negative dimension), so does this
+    short = [np.abs(rng.normal(size=(300, 12))).astype(np.float32)]
+    with pytest.raises(ValueError):
+        npo.ef_block_features(short[0], rng.normal(size=(20, 300)).astype(np.float32), np.arange(1, 300, 90))
+    with pytest.raises(ValueError):
+        _lib.ef_block_features(short, [rng.normal(size=(300, 20)).astype(np.float32)], [np.arange(1, 300, 90)])

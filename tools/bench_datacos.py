@@ -1,6 +1,12 @@
-"""One GPU's share of the Da-TACOS Serra09 configuration (BASELINE.json configs[2]).
+"""One GPU's share of the Da-TACOS configurations (BASELINE.json configs[2..4]).
 
-    python tools/bench_datacos.py [--frames 500] [--world 8] [--rank 0] [--chunk 1048576]
+    python tools/bench_datacos.py [--algo serra09|simple|earlyfusion] [--frames 500] [--world 8]
+                                  [--rank 0] [--chunk 1048576] [--max-pairs P]
+
+--algo simple: SiMPle on every ORDERED pair of the stripe (unit-column float64 features of
+--frames columns); --algo earlyfusion: the batched EarlyFusion scores of the stripe's pairs on
+synthetic block features (--frames beat blocks per track, made on the device); --max-pairs
+stops after that many pairs of the stripe (the projection uses the measured rate).
 
 Da-TACOS benchmark-shaped corpus (1000 cliques x 13 + 2000 singletons = 15,000 tracks; synthetic
 HPCP, --frames per track at the CSM input, ragged by +-10 %), the cost-balanced row stripe that
@@ -30,6 +36,8 @@ ap.add_argument("--world", type=int, default=8)
 ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--chunk", type=int, default=1 << 20)
 ap.add_argument("--tracks", type=int, default=15000)
+ap.add_argument("--algo", choices=["serra09", "simple", "earlyfusion"], default="serra09")
+ap.add_argument("--max-pairs", type=int, default=0)
 a = ap.parse_args()
 t0 = time.perf_counter()
 rng = np.random.Generator(np.random.PCG64(20250101))
@@ -48,17 +56,47 @@ tracks, labels = tracks[:a.tracks], np.asarray(labels[:a.tracks], np.int32)
 T = len(tracks)
 lens = np.array([len(t) for t in tracks], np.int32)
 print("corpus: %d tracks, frames %d..%d, %.1f s" % (T, lens.min(), lens.max(), time.perf_counter() - t0), flush=True)
-bank = ChromaBank(tracks)
-bounds = distributed.stripe_bounds(lens, a.world, symmetric=True)
+symmetric = a.algo != "simple"
+bounds = distributed.stripe_bounds(lens, a.world, symmetric=symmetric)
 r0, r1 = bounds[a.rank]
-pairs = distributed.stripe_pairs(T, r0, r1, symmetric=True)
+pairs = distributed.stripe_pairs(T, r0, r1, symmetric=symmetric)
+if a.max_pairs:
+    pairs = pairs[:a.max_pairs]
 blk = torch.zeros((r1 - r0, T), dtype=torch.float32, device="cuda")
-bank.crp_align(pairs[:4096], qmax=True)  # warm the workspaces
+if a.algo == "serra09":
+    bank = ChromaBank(tracks)
+
+    def score(ch):
+        return bank.crp_align(ch, qmax=True)["qmax"]
+elif a.algo == "simple":
+    feats = []
+    for t in tracks:
+        F = np.ascontiguousarray(np.asarray(t, np.float64).T) + 1e-3
+        feats.append(F / np.linalg.norm(F, axis=0, keepdims=True))
+    flat = torch.as_tensor(np.concatenate([f.ravel() for f in feats])).cuda()
+    off = np.concatenate([[0], np.cumsum([12 * f.shape[1] for f in feats])[:-1]]).astype(np.int64)
+
+    def score(ch):
+        sc, _ = _lib.simple_mp_packed(flat, off, lens, ch)
+        return (-sc).float()
+else:
+    NB = a.frames
+    g = torch.Generator(device="cuda").manual_seed(1)
+    ebank = {"mfccs": torch.randn((T * NB, 1000), device="cuda", generator=g),
+             "ssms": torch.rand((T * NB, 1225), device="cuda", generator=g),
+             "chromas": torch.rand((T * NB, 480), device="cuda", generator=g),
+             "chroma_med": torch.rand((T, 12), device="cuda", generator=g),
+             "off": torch.as_tensor(np.arange(T, dtype=np.int64) * NB).cuda(),
+             "nb": torch.as_tensor(np.full(T, NB, np.int32)).cuda(), "max_blocks": NB}
+
+    def score(ch):
+        return _lib.earlyfusion(ebank, ch, 0.1, 10)[:, 3].float()
+score(pairs[:1024])  # warm the workspaces
 torch.cuda.synchronize()
 t1 = time.perf_counter()
 for c0 in range(0, len(pairs), a.chunk):
     ch = pairs[c0:c0 + a.chunk]
-    q = bank.crp_align(ch, qmax=True)["qmax"]
+    q = score(ch)
     p = torch.as_tensor(ch.astype(np.int64)).cuda()
     blk[p[:, 0] - r0, p[:, 1]] = q
     torch.cuda.synchronize()
@@ -66,11 +104,11 @@ for c0 in range(0, len(pairs), a.chunk):
     el = time.perf_counter() - t1
     print("  %d / %d pairs, %.1f s, %.0f pairs/s" % (done, len(pairs), el, done / el), flush=True)
 dt = time.perf_counter() - t1
-out = {"tracks": T, "frames": a.frames, "world": a.world, "rank": a.rank, "stripe_rows": [r0, r1],
+job = T * (T - 1) // (2 if symmetric else 1)
+out = {"algo": a.algo, "tracks": T, "frames": a.frames, "world": a.world, "rank": a.rank, "stripe_rows": [r0, r1],
        "pairs": int(len(pairs)), "seconds": round(dt, 2), "pairs_per_s": round(len(pairs) / dt, 1),
-       "job_pairs": T * (T - 1) // 2,
-       "projected_job_seconds_on_world": round((T * (T - 1) // 2) / a.world / (len(pairs) / dt), 1)}
-if a.world == 1:
+       "job_pairs": job, "projected_job_seconds_on_world": round(job / a.world / (len(pairs) / dt), 1)}
+if a.world == 1 and not a.max_pairs and a.algo == "serra09":
     norm = np.sqrt(lens.astype(np.float64))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()

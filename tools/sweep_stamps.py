@@ -38,3 +38,9 @@ cols = max(out[31], 1)
 print("column select per column: search %.0f  group %.0f  threshold %.0f  le_bits+word %.0f  (%d columns)"
       % (out[32] / cols, out[33] / cols, out[34] / cols, out[35] / cols, cols))
 print("row select per row: search %.0f  group %.0f  threshold %.0f" % (out[36] / rows, out[37] / rows, out[38] / rows))
+for side, (ln, ps, gr, mem, leg, uh, uhp) in (("rows", (6, 7, 8, 9, 10, 16, 17)), ("cols", (11, 12, 13, 14, 15, 18, 19))):
+    n = max(out[ln], 1)
+    print("%s: lines %d  passes/line %.2f  group rounds/line %.2f  members/group %.2f  le-group recomputes/line %.3f  "
+          "unhinted %.3f (passes %.2f)" % (side, out[ln], out[ps] / n, out[gr] / n, out[mem] / max(out[gr], 1),
+                                           out[leg] / n, out[uh] / n, out[uhp] / max(out[uh], 1)))
+print("hint distance histogram (0,1,2,<=4,<=8,<=16,<=32,>32):", [int(out[20 + b]) for b in range(8)])
