@@ -461,6 +461,11 @@ struct Line {
     for (int h = 0; h < KPL / 2; ++h) c = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c;
     return wave_sum((int)c);
   }
+  // two probes, one wave sum: count(<= x1) in bits 0..15, count(<= x2) in bits 16..31 (each <= 2048)
+  __device__ __forceinline__ unsigned cnt_any(unsigned x) const { return in_win(x) ? cnt8(x) : cnt16(x); }
+  __device__ __forceinline__ unsigned count_le2(unsigned x1, unsigned x2) const {
+    return (unsigned)wave_sum((int)(cnt_any(x1) | (cnt_any(x2) << 16)));
+  }
   // Bit q set iff element q's prefix == P (P <= kCodeMax). Per field, (a ^ P) + 0x7fff keeps bit
   // 15 iff a != P; fields are <= 0x7fff, so nothing carries across.
   __device__ __forceinline__ bool eq_in_win(unsigned P) const {
@@ -650,6 +655,25 @@ struct LineS {
     for (int h = 0; h < KQ / 2; ++h) c = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c;
     return wave_sum((int)c);
   }
+  __device__ __forceinline__ unsigned cnt_any(unsigned x) const {
+    if constexpr (kWin) {
+      if (in_win(x)) {
+        const unsigned X4 = (x - base8 + 0x80u) * 0x01010101u;
+        unsigned c = 0;
+#pragma unroll
+        for (int h = 0; h < KQ / 4; ++h) c = __builtin_popcount((X4 - w8[h]) & 0x80808080u) + c;
+        return c;
+      }
+    }
+    const unsigned X2 = (x + 0x8000u) * 0x10001u;
+    unsigned c = 0;
+#pragma unroll
+    for (int h = 0; h < KQ / 2; ++h) c = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + c;
+    return c;
+  }
+  __device__ __forceinline__ unsigned count_le2(unsigned x1, unsigned x2) const {
+    return (unsigned)wave_sum((int)(cnt_any(x1) | (cnt_any(x2) << 16)));
+  }
   __device__ __forceinline__ uint32_t eq_mask(unsigned P) const {
     if constexpr (kWin) {
       if (in_win(P) && (P > base8 || base8 == 0u)) {  // code 0 is exact only when base8 == 0
@@ -748,6 +772,11 @@ struct Line2 {
     if (A.in_win(x)) return wave_sum((int)(A.cnt8(x) + B.cnt8(x)));
     return wave_sum((int)(A.cnt16(x) + B.cnt16(x)));
   }
+  __device__ __forceinline__ unsigned count_le2(unsigned x1, unsigned x2) const {
+    const unsigned c1 = A.in_win(x1) ? A.cnt8(x1) + B.cnt8(x1) : A.cnt16(x1) + B.cnt16(x1);
+    const unsigned c2 = A.in_win(x2) ? A.cnt8(x2) + B.cnt8(x2) : A.cnt16(x2) + B.cnt16(x2);
+    return (unsigned)wave_sum((int)(c1 | (c2 << 16)));
+  }
   __device__ __forceinline__ uint64_t eq_mask(unsigned P) const {
     if (A.eq_in_win(P)) return (uint64_t)A.eq8(P) | ((uint64_t)B.eq8(P) << 32);
     return (uint64_t)A.eq16(P) | ((uint64_t)B.eq16(P) << 32);
@@ -823,6 +852,77 @@ __device__ __forceinline__ unsigned prefix_of_rank(const LT& L, int rho, unsigne
   *less_out = c_am1;
   return a;
 }
+
+#ifdef ACOSS_SEARCH2P
+// prefix_of_rank with TWO probes per count pass (one packed wave sum): the bracket [a, b] shrinks
+// to one of three parts per pass, so the search takes fewer dependent passes (each pass is a
+// popcount chain plus a DPP reduction whose latency the wave waits out) for more VALU per pass.
+// The first pass tests "the answer is the hint" directly (probes hint - 1 and hint).
+template <class LT>
+__device__ __forceinline__ unsigned prefix_of_rank2(const LT& L, int rho, unsigned a, unsigned b, int n,
+                                                    unsigned hint, int* le_out, int* less_out, int* passes) {
+  int c_b = n, c_am1 = 0;
+  int mode = (hint != kNoHint) ? 0 : 3;  // 0 hint, 1 gallop down, 2 gallop up, 3 thirds
+  unsigned step = 2;
+  while (a < b) {
+    unsigned t1, t2;
+    if (b - a == 1) {  // one probe decides
+      const int c = (int)(L.count_le2(a, a) & 0xffffu);
+      ++*passes;
+      if (c > rho) { b = a; c_b = c; } else { a = a + 1; c_am1 = c; }
+      break;
+    }
+    if (mode == 0) {
+      const unsigned h = hint < a ? a : (hint > b ? b : hint);
+      t2 = h < b ? h : b - 1;
+      t1 = t2 > a ? t2 - 1 : a;
+      if (t1 == t2) t2 = t1 + 1;
+    } else if (mode == 1) {
+      t2 = (b - a > step) ? b - step : a + 1;
+      t1 = (t2 - a > 2 * step) ? t2 - 2 * step : a;
+    } else if (mode == 2) {
+      t1 = (b - a > step) ? a + step - 1 : a;
+      t2 = (b - 1 - t1 > 2 * step) ? t1 + 2 * step : b - 1;
+      if (t2 <= t1) t2 = t1 + 1;
+    } else {
+      const unsigned w = b - a;
+      t1 = a + w / 3;
+      t2 = a + (2 * w) / 3;
+      if (t2 <= t1) t2 = t1 + 1;
+      if (t2 > b - 1) t2 = b - 1;
+      if (t1 >= t2) t1 = t2 - 1;
+    }
+    const unsigned cc = L.count_le2(t1, t2);
+    ++*passes;
+    const int c1 = (int)(cc & 0xffffu), c2 = (int)(cc >> 16);
+    int part;
+    if (c1 > rho) {
+      b = t1;
+      c_b = c1;
+      part = 0;
+    } else if (c2 > rho) {
+      a = t1 + 1;
+      c_am1 = c1;
+      b = t2;
+      c_b = c2;
+      part = 1;
+    } else {
+      a = t2 + 1;
+      c_am1 = c2;
+      part = 2;
+    }
+    if (mode == 0)
+      mode = part == 0 ? 1 : (part == 2 ? 2 : 3);
+    else if (mode == 1)
+      mode = part == 0 ? (step <<= 2, 1) : 3;
+    else if (mode == 2)
+      mode = part == 2 ? (step <<= 2, 2) : 3;
+  }
+  *le_out = c_b;
+  *less_out = c_am1;
+  return a;
+}
+#endif
 
 // Search state carried from one line to the next of a wave's run: the previous line's answer
 // prefix and the local density (elements per prefix unit) seen around it.
@@ -1056,7 +1156,11 @@ __device__ __forceinline__ void line_threshold(const LT& L, int n, float kappa, 
     asm volatile("" ::"s"(P2), "s"(le2), "s"(less2));
   }
 #endif
+#ifdef ACOSS_SEARCH2P
+  const unsigned Pl = prefix_of_rank2(L, lo, kmin, kmax, n, hint->P, &le, &less, &passes);
+#else
   const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, hint->P, &le, &less, &passes);
+#endif
   ACOSS_STAMP(ts1);
   ACOSS_STAMP_ADD(KF::kRow ? 36 : 32, ts0, ts1);  // prefix search
   ACOSS_COUNT(KF::kRow ? 6 : 11, 1);
