@@ -45,6 +45,8 @@ SIGNATURES = {
     "acoss_binarize_rows": [_vp, _i32, _i32, _i32, _vp, _vp],
     "acoss_wcsm": [_vp, _i32, _i32, _i32, _i32, _f32, _vp, _vp],
     "acoss_snf_step": [_vp, _i32, _i32, _i32, _vp, _vp, _i32, ctypes.c_double, _vp, _i32, _vp],
+    "acoss_snf_diffuse_rows": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i32, _vp],
+    "acoss_snf_left_rows": [_vp, _i32, _i32, _i32, _vp, _vp, _i32, ctypes.c_double, _vp, _i32, _vp],
     "acoss_simple_mp": [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _vp],
     "acoss_median_downsample": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
     "acoss_simple_features": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _i64, _vp],
@@ -346,6 +348,56 @@ def snf_step(mats, skip, J, V, reg_diag, out=None, validated=False):
     rc = lib.acoss_snf_step(ptrs, len(mats), int(skip), n, _ptr(Jd), _ptr(Vd), int(Jd.shape[1]), float(reg_diag),
                             _ptr(out), 0 if validated else 1, _stream())
     _check(rc, "acoss_snf_step")
+    return out
+
+
+def _knn_dev(J, V, n, validated, what):
+    torch = _torch()
+    Jd = _dev(J, torch.int32).contiguous()
+    Vd = _dev(V, torch.float64).contiguous()
+    if Jd.shape != Vd.shape or Jd.dim() != 2 or Jd.shape[0] != n:
+        raise ValueError("%s: J and V must both be (n, K)" % what)
+    if not validated:
+        _check_knn(Jd, n)
+    return Jd, Vd
+
+
+def snf_diffuse_rows(stripes, skip, n, J, V, out=None, validated=False):
+    """First half of a row-sharded snf_step (acoss_snf_diffuse_rows): the rows of B = A . S^T
+    that belong to this rank's stripe, from the (rows, n) stripes of every matrix. The caller
+    all-gathers B's stripes and finishes with snf_left_rows."""
+    torch = _torch()
+    lib = load_library()
+    rows = int(stripes[0].shape[0]) if stripes else 0
+    for m in stripes:
+        if m.dtype != torch.float64 or not m.is_cuda or tuple(m.shape) != (rows, n) or not m.is_contiguous():
+            raise ValueError("snf_diffuse_rows: every stripe must be a contiguous (rows, n) float64 device tensor")
+    if len(stripes) < 2:
+        raise ValueError("snf_diffuse_rows: needs at least two matrices (the step averages the others)")
+    Jd, Vd = _knn_dev(J, V, n, validated, "snf_diffuse_rows")
+    if out is None:
+        out = torch.empty((rows, n), dtype=torch.float64, device=stripes[0].device)
+    ptrs = (ctypes.c_void_p * len(stripes))(*[m.data_ptr() for m in stripes])
+    rc = lib.acoss_snf_diffuse_rows(ptrs, len(stripes), int(skip), int(n), rows, _ptr(Jd), _ptr(Vd), int(Jd.shape[1]),
+                                    _ptr(out), 0 if validated else 1, _stream())
+    _check(rc, "acoss_snf_diffuse_rows")
+    return out
+
+
+def snf_left_rows(B, row0, rows, J, V, reg_diag, out=None, validated=False):
+    """Second half of a row-sharded snf_step (acoss_snf_left_rows): rows [row0, row0 + rows) of
+    S . B + reg_diag * I from the whole (n, n) B."""
+    torch = _torch()
+    lib = load_library()
+    n = int(B.shape[0])
+    if B.dtype != torch.float64 or not B.is_cuda or tuple(B.shape) != (n, n) or not B.is_contiguous():
+        raise ValueError("snf_left_rows: B must be a contiguous (n, n) float64 device tensor")
+    Jd, Vd = _knn_dev(J, V, n, validated, "snf_left_rows")
+    if out is None:
+        out = torch.empty((rows, n), dtype=torch.float64, device=B.device)
+    rc = lib.acoss_snf_left_rows(_ptr(B), n, int(row0), int(rows), _ptr(Jd), _ptr(Vd), int(Jd.shape[1]),
+                                 float(reg_diag), _ptr(out), 0 if validated else 1, _stream())
+    _check(rc, "acoss_snf_left_rows")
     return out
 
 

@@ -150,6 +150,9 @@ def _fusion_ws(Ws, K=5, niters=20, reg_diag=1):
     Vs = [S.V.to(torch.float64).contiguous() for S in Ss]
     for Jt in Js:
         _lib.check_knn(Jt, Pts[0].shape[0])
+    world, rank = _shard_world()
+    if world > 1:
+        return _fusion_sharded(Pts, Js, Vs, niters, reg_diag, world, rank)
     for it in range(niters):
         # the reference's `Pts = nextPts` aliasing: from the second iteration on, matrix i's
         # update already sees the new matrices k < i; replacing Pts[i] in place of the list
@@ -162,6 +165,55 @@ def _fusion_ws(Ws, K=5, niters=20, reg_diag=1):
     for Pt in Pts:
         Fused += Pt
     return Fused / N
+
+
+def _shard_world():
+    """(world, rank) when the fusion should row-shard across torch.distributed ranks, else
+    (1, 0). ACOSS_SNF_SHARD=0 keeps every rank on the whole matrices (replicated)."""
+    import os
+    import torch.distributed as dist
+    if os.environ.get("ACOSS_SNF_SHARD", "1") == "0":
+        return 1, 0
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def shard_rows(n, world):
+    """[(r0, r1)] per rank: equal row stripes (every row of a step costs the same, K gathered rows)."""
+    per = -(-n // world)
+    return [(min(n, r * per), min(n, (r + 1) * per)) for r in range(world)]
+
+
+def _fusion_sharded(Pts, Js, Vs, niters, reg_diag, world, rank):
+    """The cross-diffusion loop row-sharded across ranks. Rank r owns rows
+    [r0, r1) of every Pts[i]. A step for matrix i needs B = A . S^T whole but A only by rows:
+    B's rows a come from A's rows a (acoss_snf_diffuse_rows), the stripes of B are all-gathered
+    (the one exchange per step), and each rank forms its rows of S . B (acoss_snf_left_rows).
+    The loop order, the `Pts = nextPts` aliasing and every sum are those of the replicated loop,
+    so the gathered result is bit-identical to it."""
+    from ... import distributed as _dist
+    torch = _lib._torch()
+    n = Pts[0].shape[0]
+    bounds = shard_rows(n, world)
+    r0, r1 = bounds[rank]
+    if r1 <= r0:
+        raise ValueError("SNF row sharding needs at least one row per rank (n=%d, world=%d)" % (n, world))
+    St = [P[r0:r1].contiguous() for P in Pts]
+    N = len(St)
+    for it in range(niters):
+        nxt = list(St) if it == 0 else St
+        for i in range(N):
+            Bs = _lib.snf_diffuse_rows(St, i, n, Js[i], Vs[i], validated=True)
+            B = _dist.all_gather_stripes(Bs, bounds)
+            nxt[i] = _lib.snf_left_rows(B, r0, r1 - r0, Js[i], Vs[i], reg_diag, validated=True)
+            del B
+        St = nxt
+    Fused = torch.zeros_like(St[0])
+    for Pt in St:
+        Fused += Pt
+    Fused = Fused / N
+    return _dist.all_gather_stripes(Fused, bounds)
 
 
 def doSimilarityFusionWs(Ws, K=5, niters=20, reg_diag=1):

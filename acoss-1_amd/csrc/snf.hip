@@ -69,13 +69,14 @@ __global__ void k_snf_sort_knn(const int32_t* __restrict__ J, const double* __re
   }
 }
 
-// At[c, a] = (sum_{m != skip} mats[m][a, c]) / (n_mats - 1): 64 x 64 tile through LDS.
+// At[c, a] = (sum_{m != skip} mats[m][a, c]) / (n_mats - 1): 64 x 64 tile through LDS, over the
+// `rows` rows a of a row stripe (the mats are (rows, n) stripes; At is (n, rows)).
 // One launch sums a chunk of `cnt` matrices (the skipped one already left out, ascending m)
 // onto the running sum `part` (untransposed; NULL for the first chunk). A chunk that is not
 // the last writes the running sum to `part_out` untransposed; the last divides and writes At.
 // A middle chunk reads and writes the same running sum (part == part_out): each element is read
 // and then written by the same thread, and the two pointers are not __restrict__.
-__global__ __launch_bounds__(256) void k_snf_avg_t(MatPtrs mats, int32_t cnt, int32_t n, double denom,
+__global__ __launch_bounds__(256) void k_snf_avg_t(MatPtrs mats, int32_t cnt, int32_t rows, int32_t n, double denom,
                                                    const double* part, double* part_out,
                                                    double* __restrict__ At) {
   __shared__ double tile[64][65];
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(256) void k_snf_avg_t(MatPtrs mats, int32_t cnt, in
     const int idx = t + 256 * r;
     const int a = a0 + (idx >> 6), c = c0 + (idx & 63);
     double s = 0.0;
-    if (a < n && c < n) {
+    if (a < rows && c < n) {
       const int64_t e = (int64_t)a * n + c;
       if (part) s = part[e];
       for (int m = 0; m < cnt; ++m) s = s + mats.p[m][e];
@@ -103,23 +104,24 @@ __global__ __launch_bounds__(256) void k_snf_avg_t(MatPtrs mats, int32_t cnt, in
   for (int r = 0; r < 16; ++r) {
     const int idx = t + 256 * r;
     const int c = c0 + (idx >> 6), a = a0 + (idx & 63);
-    if (a < n && c < n) At[(int64_t)c * n + a] = tile[idx >> 6][idx & 63];
+    if (a < rows && c < n) At[(int64_t)c * rows + a] = tile[idx >> 6][idx & 63];
   }
 }
 
-// B[a, j] = sum_k Vs[j,k] * At[Js[j,k], a]. Block = 32 rows j x 64 columns a; each wave takes
+// B[a, j] = sum_k Vs[j,k] * At[Js[j,k], a] for the stripe's rows a < rows (At is (n, rows), B
+// the (rows, n) stripe of the product). Block = 32 rows j x 64 columns a; each wave takes
 // 8 rows j, lane = column a (each gathered row segment is one 512-byte run), and the 32 x 64
 // result leaves transposed through LDS as 64 runs of 32 doubles. (16-byte loads over 128
 // columns measured slower: 17.2 vs 16.4 ms per step at n = 15,000.)
 constexpr int kGJ = 32;
-__global__ __launch_bounds__(256) void k_snf_gather_t(const double* __restrict__ At, int32_t n, int32_t K,
+__global__ __launch_bounds__(256) void k_snf_gather_t(const double* __restrict__ At, int32_t rows, int32_t n, int32_t K,
                                                       const int32_t* __restrict__ Js,
                                                       const double* __restrict__ Vs, double* __restrict__ B) {
   __shared__ double tile[64][kGJ + 1];
   const int a0 = blockIdx.x * 64, j0 = blockIdx.y * kGJ;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int a = a0 + lane;
-  const bool aok = a < n;
+  const bool aok = a < rows;
 #pragma unroll
   for (int q = 0; q < kGJ / 4; ++q) {
     const int jl = w * (kGJ / 4) + q;
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(256) void k_snf_gather_t(const double* __restrict__
       for (int k = 0; k < K; ++k) {
         const int32_t row = Js[(int64_t)j * K + k];
         const double v = Vs[(int64_t)j * K + k];
-        if (aok) acc = acc + v * At[(int64_t)row * n + a];
+        if (aok) acc = acc + v * At[(int64_t)row * rows + a];
       }
     }
     tile[lane][jl] = acc;
@@ -140,17 +142,18 @@ __global__ __launch_bounds__(256) void k_snf_gather_t(const double* __restrict__
     const int idx = threadIdx.x + 256 * r;
     const int al = idx / kGJ, jl = idx % kGJ;
     const int aa = a0 + al, j = j0 + jl;
-    if (aa < n && j < n) B[(int64_t)aa * n + j] = tile[al][jl];
+    if (aa < rows && j < n) B[(int64_t)aa * n + j] = tile[al][jl];
   }
 }
 
 // out[i, j] = sum_k Vs[i,k] * B[Js[i,k], j] (+ reg_diag on the diagonal, added after the sum
-// as the reference's separate `nextPts[i][pix, pix] += reg_diag`). Block = row i x 1024 columns,
-// 4 consecutive columns per thread as two 16-byte loads per gathered row.
-__global__ __launch_bounds__(256) void k_snf_left(const double* __restrict__ B, int32_t n, int32_t K,
+// as the reference's separate `nextPts[i][pix, pix] += reg_diag`) for the rows i of the stripe
+// [row0, row0 + gridDim.y); out is that (rows, n) stripe, B the whole (n, n) product.
+// Block = row i x 1024 columns, 4 consecutive columns per thread as two 16-byte loads per row.
+__global__ __launch_bounds__(256) void k_snf_left(const double* __restrict__ B, int32_t n, int32_t row0, int32_t K,
                                                   const int32_t* __restrict__ Js, const double* __restrict__ Vs,
                                                   double reg_diag, double* __restrict__ out) {
-  const int i = blockIdx.y;
+  const int i = row0 + blockIdx.y;
   const int j0 = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (j0 >= n) return;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(256) void k_snf_left(const double* __restrict__ B, 
         if (j0 + t < n) acc[t] = acc[t] + v * src[t];
     }
   }
-  double* dst = out + (int64_t)i * n + j0;
+  double* dst = out + (int64_t)blockIdx.y * n + j0;
   for (int t = 0; t < 4; ++t) {
     const int j = j0 + t;
     if (j < n) {
@@ -187,12 +190,80 @@ __global__ __launch_bounds__(256) void k_snf_left(const double* __restrict__ B, 
 
 using namespace acoss;
 
+namespace {
+
+bool snf_args_ok(const int32_t* J, const double* V, int32_t n, int32_t K) {
+  return n > 0 && J && V && K > 0 && K <= kSnfMaxK && K <= n;
+}
+
+// Sorts the kNN rows into csr order (Js, Vs in workspace slot 12, after `lead` bytes) and, with
+// `validate`, checks them (one stream sync) before any product reads a row they name. Without it
+// a bad row has already been made harmless (its own column, weight 0), so no kernel reads
+// outside the matrices; a caller that validated J once per fusion skips the sync.
+int snf_sorted_knn(const int32_t* J, const double* V, int32_t n, int32_t K, int32_t validate, size_t lead,
+                   hipStream_t s, char** ws_out, int32_t** Js, double** Vs) {
+  const size_t knn = align_up((size_t)n * K, 64);
+  char* ws = static_cast<char*>(workspace(12, lead + knn * 12 + 512));
+  if (!ws) return ACOSS_E_HIP;
+  *Vs = reinterpret_cast<double*>(ws + lead);
+  *Js = reinterpret_cast<int32_t*>(ws + lead + knn * 8);
+  int32_t* d_err = reinterpret_cast<int32_t*>(ws + lead + knn * 12);
+  ACOSS_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
+  hipLaunchKernelGGL(k_snf_sort_knn, dim3((n + 255) / 256), dim3(256), 0, s, J, V, n, K, *Js, *Vs, d_err);
+  ACOSS_LAUNCH_CHECK();
+  if (validate) {
+    int h_err = 0;
+    ACOSS_HIP_CHECK(hipMemcpyAsync(&h_err, d_err, 4, hipMemcpyDeviceToHost, s));
+    ACOSS_HIP_CHECK(hipStreamSynchronize(s));
+    if (h_err) {
+      set_error("acoss_snf: kNN column indices must lie in [0, %d) without repeats within a row", n);
+      return ACOSS_E_ARG;
+    }
+  }
+  *ws_out = ws;
+  return ACOSS_OK;
+}
+
+// B = (S . At)^T over a (rows, n) row stripe of the average of the other matrices: the average
+// in the reference's order (m ascending, chunks of kSnfChunk pointers, one division), its
+// transpose At (n x rows), then the gather. A multi-chunk running sum lives in B (free until
+// the gather writes it).
+int snf_diffuse(const double* const* mats, int32_t n_mats, int32_t skip, int32_t n, int32_t rows,
+                const int32_t* Js, const double* Vs, int32_t K, double* At, double* B, hipStream_t s) {
+  const double denom = (double)(n_mats - 1);
+  const unsigned nc = (unsigned)((n + 63) / 64), nr = (unsigned)((rows + 63) / 64);
+  MatPtrs mp{};
+  int cnt = 0, done = 0;
+  const double* part = nullptr;
+  for (int m = 0; m < n_mats; ++m) {
+    if (m == skip) continue;
+    mp.p[cnt++] = mats[m];
+    ++done;
+    if (cnt == kSnfChunk || done == n_mats - 1) {
+      const bool last = done == n_mats - 1;
+      hipLaunchKernelGGL(k_snf_avg_t, dim3(nc, nr), dim3(256), 0, s, mp, cnt, rows, n, denom, part,
+                         last ? nullptr : B, At);
+      ACOSS_LAUNCH_CHECK();
+      part = B;
+      cnt = 0;
+    }
+  }
+  hipLaunchKernelGGL(k_snf_gather_t, dim3(nr, (n + kGJ - 1) / kGJ), dim3(256), 0, s, At, rows, n, K, Js, Vs, B);
+  ACOSS_LAUNCH_CHECK();
+  return ACOSS_OK;
+}
+
+bool overlaps(const double* a, size_t na, const double* b, size_t nb) {
+  return a < b + nb && b < a + na;
+}
+
+}  // namespace
+
 extern "C" int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t skip, int32_t n,
                               const int32_t* J, const double* V, int32_t K, double reg_diag, double* out,
                               int32_t validate, void* hip_stream) {
   clear_error();
-  if (!mats || n_mats < 2 || skip < 0 || skip >= n_mats || n <= 0 || !J || !V || !out || K <= 0 ||
-      K > kSnfMaxK || K > n) {
+  if (!mats || n_mats < 2 || skip < 0 || skip >= n_mats || !out || !snf_args_ok(J, V, n, K)) {
     set_error("acoss_snf_step: bad arguments (need n_mats >= 2, 0 <= skip < n_mats, 0 < K <= min(n, %d))",
               kSnfMaxK);
     return ACOSS_E_ARG;
@@ -205,52 +276,67 @@ extern "C" int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t
   }
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   const size_t nn = (size_t)n * n;
-  const size_t knn = align_up((size_t)n * K, 64);
-  char* ws = static_cast<char*>(workspace(12, 2 * nn * 8 + knn * 12 + 512));
-  if (!ws) return ACOSS_E_HIP;
+  char* ws = nullptr;
+  int32_t* Js = nullptr;
+  double* Vs = nullptr;
+  int rc = snf_sorted_knn(J, V, n, K, validate, 2 * nn * 8, s, &ws, &Js, &Vs);
+  if (rc != ACOSS_OK) return rc;
   double* Bm = reinterpret_cast<double*>(ws);
   double* At = reinterpret_cast<double*>(ws + nn * 8);
-  double* Vs = reinterpret_cast<double*>(ws + 2 * nn * 8);
-  int32_t* Js = reinterpret_cast<int32_t*>(ws + 2 * nn * 8 + knn * 8);
-  int32_t* d_err = reinterpret_cast<int32_t*>(ws + 2 * nn * 8 + knn * 12);
-  const unsigned nt = (unsigned)((n + 63) / 64);
-  ACOSS_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
-  hipLaunchKernelGGL(k_snf_sort_knn, dim3((n + 255) / 256), dim3(256), 0, s, J, V, n, K, Js, Vs, d_err);
+  rc = snf_diffuse(mats, n_mats, skip, n, n, Js, Vs, K, At, Bm, s);
+  if (rc != ACOSS_OK) return rc;
+  hipLaunchKernelGGL(k_snf_left, dim3((n + 1023) / 1024, n), dim3(256), 0, s, Bm, n, 0, K, Js, Vs, reg_diag, out);
   ACOSS_LAUNCH_CHECK();
-  // validate: the kNN columns are checked (one stream sync) before any product reads a row they
-  // name. Without it a bad row has already been made harmless (its own column, weight 0), so no
-  // kernel reads outside the matrices; a caller that validated J once per fusion skips the sync.
-  if (validate) {
-    int h_err = 0;
-    ACOSS_HIP_CHECK(hipMemcpyAsync(&h_err, d_err, 4, hipMemcpyDeviceToHost, s));
-    ACOSS_HIP_CHECK(hipStreamSynchronize(s));
-    if (h_err) {
-      set_error("acoss_snf_step: kNN column indices must lie in [0, %d) without repeats within a row", n);
+  return ACOSS_OK;
+}
+
+extern "C" int acoss_snf_diffuse_rows(const double* const* mats, int32_t n_mats, int32_t skip, int32_t n,
+                                      int32_t rows, const int32_t* J, const double* V, int32_t K, double* B_rows,
+                                      int32_t validate, void* hip_stream) {
+  clear_error();
+  if (!mats || n_mats < 2 || skip < 0 || skip >= n_mats || rows <= 0 || rows > n || !B_rows ||
+      !snf_args_ok(J, V, n, K)) {
+    set_error("acoss_snf_diffuse_rows: bad arguments (need n_mats >= 2, 0 <= skip < n_mats, 0 < rows <= n, "
+              "0 < K <= min(n, %d))", kSnfMaxK);
+    return ACOSS_E_ARG;
+  }
+  const size_t sn = (size_t)rows * n;
+  for (int m = 0; m < n_mats; ++m) {
+    if (!mats[m] || (m != skip && overlaps(mats[m], sn, B_rows, sn))) {
+      set_error("acoss_snf_diffuse_rows: stripe %d is NULL or overlaps the output", m);
       return ACOSS_E_ARG;
     }
   }
-  // average of the other matrices, ascending m, in chunks of kSnfChunk pointers; the running
-  // sum of a multi-chunk average lives in Bm (free until the first product)
-  const double denom = (double)(n_mats - 1);
-  MatPtrs mp{};
-  int cnt = 0, done = 0;
-  const double* part = nullptr;
-  for (int m = 0; m < n_mats; ++m) {
-    if (m == skip) continue;
-    mp.p[cnt++] = mats[m];
-    ++done;
-    if (cnt == kSnfChunk || done == n_mats - 1) {
-      const bool last = done == n_mats - 1;
-      hipLaunchKernelGGL(k_snf_avg_t, dim3(nt, nt), dim3(256), 0, s, mp, cnt, n, denom, part,
-                         last ? nullptr : Bm, At);
-      ACOSS_LAUNCH_CHECK();
-      part = Bm;
-      cnt = 0;
-    }
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  char* ws = nullptr;
+  int32_t* Js = nullptr;
+  double* Vs = nullptr;
+  int rc = snf_sorted_knn(J, V, n, K, validate, sn * 8, s, &ws, &Js, &Vs);
+  if (rc != ACOSS_OK) return rc;
+  return snf_diffuse(mats, n_mats, skip, n, rows, Js, Vs, K, reinterpret_cast<double*>(ws), B_rows, s);
+}
+
+extern "C" int acoss_snf_left_rows(const double* B, int32_t n, int32_t row0, int32_t rows, const int32_t* J,
+                                   const double* V, int32_t K, double reg_diag, double* out, int32_t validate,
+                                   void* hip_stream) {
+  clear_error();
+  if (!B || !out || row0 < 0 || rows <= 0 || rows > n - row0 || !snf_args_ok(J, V, n, K)) {
+    set_error("acoss_snf_left_rows: bad arguments (need 0 <= row0, 0 < rows <= n - row0, 0 < K <= min(n, %d))",
+              kSnfMaxK);
+    return ACOSS_E_ARG;
   }
-  hipLaunchKernelGGL(k_snf_gather_t, dim3(nt, (n + kGJ - 1) / kGJ), dim3(256), 0, s, At, n, K, Js, Vs, Bm);
-  ACOSS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_snf_left, dim3((n + 1023) / 1024, n), dim3(256), 0, s, Bm, n, K, Js, Vs, reg_diag, out);
+  if (overlaps(B, (size_t)n * n, out, (size_t)rows * n)) {
+    set_error("acoss_snf_left_rows: the output overlaps B");
+    return ACOSS_E_ARG;
+  }
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  char* ws = nullptr;
+  int32_t* Js = nullptr;
+  double* Vs = nullptr;
+  int rc = snf_sorted_knn(J, V, n, K, validate, 0, s, &ws, &Js, &Vs);
+  if (rc != ACOSS_OK) return rc;
+  hipLaunchKernelGGL(k_snf_left, dim3((n + 1023) / 1024, rows), dim3(256), 0, s, B, n, row0, K, Js, Vs, reg_diag,
+                     out);
   ACOSS_LAUNCH_CHECK();
   return ACOSS_OK;
 }

@@ -133,6 +133,23 @@ int acoss_wcsm(const float* CSM, int32_t M, int32_t N, int32_t k1, int32_t k2, f
 int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t skip, int32_t n, const int32_t* J,
                    const double* V, int32_t K, double reg_diag, double* out, int32_t validate, void* hip_stream);
 
+/* The same step split at its one exchange point, for a fusion row-sharded across ranks (SURVEY
+ * §8f row 2: each rank owns rows [row0, row0 + rows) of every matrix; the same loop body,
+ * similarity_fusion.py:163-174). Both halves are bit-identical to the matching rows of
+ * acoss_snf_step: same kernels, same summation order.
+ *   acoss_snf_diffuse_rows: B_rows = rows [row0, row0 + rows) of B = A . S^T, from the (rows x n)
+ *     stripes mats[m] of the matrices (HOST array of device pointers); B_rows (rows x n) may
+ *     overlap mats[skip] but no other stripe.
+ *   (the caller all-gathers the stripes of B into the whole (n x n) B)
+ *   acoss_snf_left_rows: out = rows [row0, row0 + rows) of S . B + reg_diag * I, from the whole
+ *     (n x n) B; out (rows x n) must not overlap B.
+ * J, V, K, validate as for acoss_snf_step (J, V describe all n rows of S in both calls). */
+int acoss_snf_diffuse_rows(const double* const* mats, int32_t n_mats, int32_t skip, int32_t n, int32_t rows,
+                           const int32_t* J, const double* V, int32_t K, double* B_rows, int32_t validate,
+                           void* hip_stream);
+int acoss_snf_left_rows(const double* B, int32_t n, int32_t row0, int32_t rows, const int32_t* J, const double* V,
+                        int32_t K, double reg_diag, double* out, int32_t validate, void* hip_stream);
+
 /* SiMPle matrix profile score (A11, acoss/algorithms/simple_silva.py:68-118) for a batch of
  * ordered pairs, including the per-pair OTI roll of the reference (Simple.oti, :45-54).
  * feats: packed (12 x n_t) float64 blocks, track t at element offset track_off[t] (dim-major,

@@ -28,10 +28,14 @@ def main():
         a = Serra09(csv, fdir, shortname="mr", cachedir=cachedir)
         a.all_pairwise(symmetric=True)
         a.normalize_by_length()
-    elif algo == "ChenFusion":
+    elif algo in ("ChenFusion", "ChenLate"):
         from acoss.algorithms.latefusion_chen import ChenFusion
         a = ChenFusion(csv, fdir, shortname="mr", cachedir=cachedir)
         a.all_pairwise(symmetric=True)
+        if algo == "ChenLate":
+            # SNF late fusion (latefusion_chen.py:87-91): row-sharded across the ranks
+            a.normalize_by_length()
+            a.do_late_fusion()
     else:
         from acoss.algorithms.simple_silva import Simple
         a = Simple(csv, fdir, shortname="mr", cachedir=cachedir)

@@ -2,6 +2,7 @@
 row stripe of a Da-TACOS-shaped mini corpus (13-song cliques plus singletons, ragged
 lengths) through Serra09 / ChenFusion / Simple.all_pairwise (algorithm_template.py:142-193),
 all-gather, symmetrise on the device; the assembled Ds must equal the world-1 run bit for bit.
+ChenFusion's SNF late fusion runs row-sharded across the same two ranks.
 Ranks are child processes (subprocess), one GPU context each (3 with the parent)."""
 import os
 import socket
@@ -75,4 +76,17 @@ def test_world2_equals_world1(datacos_mini, algo):
     for k in d1:
         assert d1[k].shape == (48, 48)
         assert np.count_nonzero(d1[k]) > 48 * 30
+        np.testing.assert_array_equal(d2[k], d1[k])
+
+
+def test_late_fusion_sharded_equals_world1(datacos_mini):
+    """ChenFusion's SNF late fusion (20 cross-diffusion steps per matrix) row-sharded over two
+    ranks — one all-gather of B per step (similarity_fusion._fusion_sharded) — equals the
+    single-process fusion bit for bit."""
+    root, csv, fdir = datacos_mini
+    d1 = _run("ChenLate", 1, root, csv, fdir, "a")
+    d2 = _run("ChenLate", 2, root, csv, fdir, "b")
+    assert set(d1) == set(d2) and "Late" in d1
+    assert np.count_nonzero(d1["Late"]) > 48 * 30
+    for k in d1:
         np.testing.assert_array_equal(d2[k], d1[k])

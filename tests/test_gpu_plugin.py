@@ -213,6 +213,39 @@ def test_snf_step_many_matrices():
         np.testing.assert_array_equal(got, npo.snf_step(mats, skip, J, V, 1.0))
 
 
+@pytest.mark.parametrize("n,K,L,world", [(40, 5, 2, 2), (333, 20, 3, 3), (1030, 7, 4, 8), (70, 6, 19, 4)])
+def test_snf_rows_split_bitexact(n, K, L, world):
+    """The row-sharded step (acoss_snf_diffuse_rows, gather, acoss_snf_left_rows) stripe by
+    stripe equals acoss_snf_step and the scipy expression, for ragged last stripes and more
+    matrices than one argument chunk."""
+    import torch
+    from acoss.algorithms.utils.similarity_fusion import shard_rows
+    rng = np.random.default_rng(n + L)
+    mats = [rng.random((n, n)) for _ in range(L)]
+    J = np.stack([rng.choice(n, K, replace=False) for _ in range(n)]).astype(np.int32)
+    V = rng.random((n, K))
+    dm = [torch.as_tensor(m).cuda() for m in mats]
+    bounds = shard_rows(n, world)
+    for skip in sorted({0, L - 1}):
+        ref = npo.snf_step(mats, skip, J, V, 1.0)
+        Bs = [_lib.snf_diffuse_rows([m[r0:r1].contiguous() for m in dm], skip, n, J, V) for r0, r1 in bounds]
+        B = torch.cat(Bs, 0).contiguous()
+        got = torch.cat([_lib.snf_left_rows(B, r0, r1 - r0, J, V, 1.0) for r0, r1 in bounds], 0).cpu().numpy()
+        np.testing.assert_array_equal(got, ref)
+        np.testing.assert_array_equal(_lib.snf_step(dm, skip, J, V, 1.0).cpu().numpy(), ref)
+    # the output stripe may reuse the skipped matrix's stripe; other overlaps are refused
+    st = [m[:7].contiguous() for m in dm]
+    want = _lib.snf_diffuse_rows(st, 0, n, J, V).clone()
+    np.testing.assert_array_equal(_lib.snf_diffuse_rows(st, 0, n, J, V, out=st[0]).cpu().numpy(), want.cpu().numpy())
+    with pytest.raises(_lib.AcossHipError):
+        _lib.snf_diffuse_rows(st, 0, n, J, V, out=st[1])
+    B = torch.zeros((n, n), dtype=torch.float64, device="cuda")
+    with pytest.raises(_lib.AcossHipError):
+        _lib.snf_left_rows(B, 0, 3, J, V, 1.0, out=B[5:8])
+    with pytest.raises(_lib.AcossHipError):
+        _lib.snf_left_rows(B, n - 2, 3, J, V, 1.0)
+
+
 def test_snf_float32_matches_restatement():
     """doSimilarityFusion on float32 distance matrices (the ChenFusion / EarlyFusion input dtype)
     vs the numpy restatement at the stated SNF tolerance, with an inf diagonal as Chen has."""
