@@ -1096,17 +1096,9 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   int64_t sub = nb_alloc;
   // split sub-batch scratch per pair: 16-bit prefixes row-major and strip-major (2 + 2 B per
   // cell) and the row-threshold words RT
-#if defined(ACOSS_LO_PLANE) || defined(ACOSS_FK_ROWS)
-  const size_t sub_pair = 6 * (size_t)kstride + 4 * (size_t)mask_stride;  // + the low-half plane
-#else
   const size_t sub_pair = 4 * (size_t)kstride + 4 * (size_t)mask_stride;
-#endif
   if (split) {
-#if defined(ACOSS_LO_PLANE) || defined(ACOSS_FK_ROWS)
-    size_t kbudget = (size_t)3 << 29;  // 1.5 GB: the same ~63 pairs per sub-batch with the third plane
-#else
-    size_t kbudget = (size_t)1 << 30;  // ~63 pairs at 2000 frames (x2 buffers): fills 256 CUs per launch
-#endif
+    size_t kbudget = (size_t)1 << 30;  // ~42 pairs at 2000 frames (x2 buffers): fills 256 CUs per launch
     if (const char* e = getenv("ACOSS_KEY_BYTES")) kbudget = strtoull(e, nullptr, 10);
     sub = (int64_t)(kbudget / sub_pair);
     if (sub < 1) sub = 1;
@@ -1141,11 +1133,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   void* w_kpl[3] = {nullptr, nullptr, nullptr};
   uint32_t* w_rt[3] = {nullptr, nullptr, nullptr};
   for (int b = 0; split && b < nbuf; ++b) {
-#if defined(ACOSS_LO_PLANE) || defined(ACOSS_FK_ROWS)
-    w_kpl[b] = static_cast<void*>(carve(6 * (size_t)kstride * sub));
-#else
     w_kpl[b] = static_cast<void*>(carve(4 * (size_t)kstride * sub));
-#endif
     w_rt[b] = reinterpret_cast<uint32_t*>(carve(4 * (size_t)mask_stride * sub));
   }
   // row-major key plane as per-XCD rings of strip slots (HrRing, crp_split.hip): ACOSS_HR_RING =

@@ -88,7 +88,6 @@ struct KeyPlanes {
   uint16_t* hr;
   uint16_t* hc;
   HrRing ring;
-  uint16_t* lo;  // ACOSS_LO_PLANE: low 16 bits of every key, row-major per pair (pitch ldr)
 };
 
 // Exact key of cell (i, j), recomputed in the sweep's canonical order: 12-term fmaf chain per
@@ -139,20 +138,6 @@ struct LineCells {
   __device__ __forceinline__ int qi(int e) const { return ROW ? fix : e; }
   __device__ __forceinline__ int rj(int e) const { return ROW ? e : fix; }
   __device__ __forceinline__ unsigned operator()(int e) const { return cell_key(V, qi(e), rj(e)); }
-#if defined(ACOSS_FK_ROWS)
-  const uint32_t* fk;  // the pair's full-key row-major plane (pitch ldr)
-  int ldr;
-  __device__ __forceinline__ unsigned key_p(int e, unsigned) const { return fk[(int64_t)qi(e) * ldr + rj(e)]; }
-#elif defined(ACOSS_LO_PLANE)
-  const uint16_t* lo;  // the pair's low-half plane (row-major, pitch ldr)
-  int ldr;
-  // exact key of element e whose 16-bit prefix is P: prefix | stored low half (no recompute)
-  __device__ __forceinline__ unsigned key_p(int e, unsigned P) const {
-    return (P << 16) | (unsigned)lo[(int64_t)qi(e) * ldr + rj(e)];
-  }
-#else
-  __device__ __forceinline__ unsigned key_p(int e, unsigned) const { return (*this)(e); }
-#endif
 };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -168,12 +153,6 @@ __device__ __forceinline__ void st_u16(gu16* base, unsigned idx, unsigned v) {
 #endif
   typedef __attribute__((address_space(1))) char gchar;
   *(gu16*)((gchar*)base + idx * 2u) = (uint16_t)v;
-}
-
-typedef __attribute__((address_space(1))) uint32_t gu32_t;
-__device__ __forceinline__ void st_u32(gu32_t* base, unsigned idx, unsigned v) {
-  typedef __attribute__((address_space(1))) char gchar;
-  *(gu32_t*)((gchar*)base + idx * 4u) = v;
 }
 
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
@@ -259,12 +238,6 @@ __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int str
     const unsigned hcol = valid ? (unsigned)col : (unsigned)(ldr - 1);
     const float ny = valid ? V.NXr[col] : 0.0f;
     gu16* hrow = (gu16*)Hr;
-#ifdef ACOSS_FK_ROWS
-    gu32_t* frow = (gu32_t*)reinterpret_cast<uint32_t*>(Hr);  // Hr points at the strip of the full-key plane
-#endif
-#ifdef ACOSS_LO_PLANE
-    gu16* lrow = (gu16*)(K.lo + (size_t)p * kstride + (size_t)i0 * ldr);
-#endif
     float A[kMS];  // A[u]: window of row kk - u after u + 1 terms
     unsigned kh[16];    // rows 0..15: full keys until their split partner (row + 16) is done
     unsigned hw[16];    // split-order words: rows (h, h + 16)
@@ -296,40 +269,15 @@ __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int str
         unsigned k0 = __builtin_bit_cast(unsigned, d2.x > 0.0f ? d2.x : 0.0f);
         unsigned k1 = __builtin_bit_cast(unsigned, d2.y > 0.0f ? d2.y : 0.0f);
         if (!PARTIAL || r + 1 < rows) {  // wave-uniform; rows past M' are never stored
-#ifdef ACOSS_FK_ROWS
-          st_u32(frow, hcol, k0);
-          st_u32(frow, (unsigned)ldr + hcol, k1);
-#else
           st_u16(hrow, hcol, k0 >> 16);
           st_u16(hrow, (unsigned)ldr + hcol, k1 >> 16);
-#endif
-#ifdef ACOSS_LO_PLANE
-          st_u16(lrow, hcol, k0);
-          st_u16(lrow, (unsigned)ldr + hcol, k1);
-#endif
         } else {
-#ifdef ACOSS_FK_ROWS
-          if (r < rows) st_u32(frow, hcol, k0);
-#else
           if (r < rows) st_u16(hrow, hcol, k0 >> 16);
-#endif
-#ifdef ACOSS_LO_PLANE
-          if (r < rows) st_u16(lrow, hcol, k0);
-#endif
           if (r >= rows) k0 = kNone << 16;  // and read as "no element" in the column plane
           k1 = kNone << 16;
         }
-#ifdef ACOSS_FK_ROWS
-        frow += 2 * ldr;
-        asm volatile("" : "+s"(frow));
-#else
         hrow += 2 * ldr;
         asm volatile("" : "+s"(hrow));
-#endif
-#ifdef ACOSS_LO_PLANE
-        lrow += 2 * ldr;
-        asm volatile("" : "+s"(lrow));
-#endif
         if (r < 16) {
           kh[r] = k0;
           kh[r + 1] = k1;
@@ -364,11 +312,7 @@ __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int str
   const int padw = (int)((V.Np + 31) & ~31) - V.Np;
   for (int e = threadIdx.x; e < kSR * 32; e += kThreads) {
     const int r = e >> 5, c = e & 31;
-#ifdef ACOSS_FK_ROWS
-    if (c < padw && r < rows) reinterpret_cast<uint32_t*>(Hr)[(size_t)r * ldr + V.Np + c] = kNone << 16;
-#else
     if (c < padw && r < rows) Hr[(size_t)r * ldr + V.Np + c] = (uint16_t)kNone;
-#endif
   }
 }
 
@@ -480,30 +424,6 @@ struct Line {
     }
     // the planes hold kNone past the line's end inside the last run (the sweep stores it), so
     // only lanes wholly past the line need filling
-    if (base >= n) {
-#pragma unroll
-      for (int h = 0; h < KPL / 2; ++h) pv[h] = kNone * 0x10001u;
-    }
-  }
-  // Lane l's 32 elements from a row of FULL keys (ACOSS_FK_ROWS): 8 x 16 B per lane, the split-order
-  // words from the keys' high halves (one v_perm per word, as the 16-bit row loads)
-  __device__ __forceinline__ void load_full(const uint32_t* row, int n) {
-    const int lane = threadIdx.x & 63;
-    const int base = lane * KPL;
-    const uint32_t* src = row + (base < n ? (size_t)base : (size_t)0);
-    win = false;
-    base8 = 0u;
-    unsigned k[KPL];
-#pragma unroll
-    for (int q = 0; q < KPL / 4; ++q) {
-      const uint4 v = reinterpret_cast<const uint4*>(src)[q];
-      k[4 * q + 0] = v.x;
-      k[4 * q + 1] = v.y;
-      k[4 * q + 2] = v.z;
-      k[4 * q + 3] = v.w;
-    }
-#pragma unroll
-    for (int h = 0; h < KPL / 2; ++h) pv[h] = __builtin_amdgcn_perm(k[h + 16], k[h], 0x07060302u);
     if (base >= n) {
 #pragma unroll
       for (int h = 0; h < KPL / 2; ++h) pv[h] = kNone * 0x10001u;
@@ -709,10 +629,6 @@ struct LineS {
     unsigned v[KQ];
 #pragma unroll
     for (int q = 0; q < KQ; ++q) v[q] = *addr(min(lane + 64 * q, n - 1));
-    if constexpr (sizeof(*addr(0)) == 4) {  // full 32-bit keys (ACOSS_FK_ROWS row plane): their prefixes
-#pragma unroll
-      for (int q = 0; q < KQ; ++q) v[q] >>= 16;
-    }
 #pragma unroll
     for (int q = 0; q < KQ; ++q) v[q] = lane + 64 * q < n ? v[q] : kNone;
 #pragma unroll
@@ -968,19 +884,6 @@ __device__ __forceinline__ Group group_keys(const LT& L, unsigned P, int g, cons
     m &= m - 1;
   }
   __builtin_amdgcn_wave_barrier();
-#if defined(ACOSS_LO_PLANE) || defined(ACOSS_FK_ROWS)
-  {  // each member's key is stored (low-half plane or full-key rows): one load per lane, no Gram terms
-    const int e_me = W.list[lane < g ? lane : 0];
-    Group G;
-    G.P = P;
-    G.g = g;
-    G.elem = lane < g ? e_me : 0;
-    const unsigned k = keyf.key_p(e_me, P);
-    G.key = lane < g ? k : 0xffffffffu;
-    __builtin_amdgcn_wave_barrier();
-    return G;
-  }
-#endif
   // this lane's member (lanes >= g take member 0: a valid cell) and its two stacked norms,
   // requested before the Gram rounds so that their latency overlaps them
   const int e_me = W.list[lane < g ? lane : 0];
@@ -1103,7 +1006,7 @@ __device__ __forceinline__ unsigned big_group_rank(const LT& L, unsigned P, int 
     for (int b = lane; b < 256; b += 64) hist[b] = 0u;
     __builtin_amdgcn_wave_barrier();
     group_rounds(L, P, g, W, [&](int e) {
-      const unsigned k = keyf.key_p(e, P);
+      const unsigned k = keyf(e);
       if (pass == 0)
         atomicAdd(&hist[(k >> 8) & 0xffu], 1u);
       else if (((k >> 8) & 0xffu) == hi8)
@@ -1243,7 +1146,7 @@ __device__ __forceinline__ auto le_bits(const LT& L, unsigned Tbits, const KF& k
       if (lane < G.g && G.key > Tbits) atomicAnd(&W.words[LT::lane_of(G.elem)], ~(1u << LT::bit_of(G.elem)));
     } else {  // large group: member keys in rounds of 64
       group_rounds(L, T16, g, W, [&](int e) {
-        if (keyf.key_p(e, T16) > Tbits) atomicAnd(&W.words[LT::lane_of(e)], ~(1u << LT::bit_of(e)));
+        if (keyf(e) > Tbits) atomicAnd(&W.words[LT::lane_of(e)], ~(1u << LT::bit_of(e)));
       });
     }
   }
@@ -1303,7 +1206,7 @@ struct LineOf<2> {
 
 template <int NW, int KQ, int RB>
 __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, const uint16_t* Hr, int ldr,
-                                          const uint16_t* Klo, int64_t kstride, float kappa, float* __restrict__ thr,
+                                          float kappa, float* __restrict__ thr,
                                           float* __restrict__ Tq, int64_t thr_stride, uint32_t* __restrict__ RT,
                                           int64_t rt_stride, int ld, WaveLds* wl, uint32_t (*rowbits)[RB]) {
   using LT = typename LineOf<KQ>::T;
@@ -1316,17 +1219,6 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
   auto load_row = [&](LT& Ld, int i) {
     int64_t rowoff = (int64_t)(i - i0) * ldr;
     asm volatile("" : "+s"(rowoff));  // per-row address: nothing per lane hoisted out of the loop
-#ifdef ACOSS_FK_ROWS
-    const uint32_t* frow = reinterpret_cast<const uint32_t*>(Hr) + rowoff;
-    if constexpr (KQ == 0) {
-      Ld.load_full(frow, V.Np);
-    } else if constexpr (KQ == 2) {
-      Ld.A.load_full(frow, V.Np);
-      Ld.B.load_full(frow + 2048, V.Np - 2048);
-    } else {
-      Ld.load([&](int e) { return frow + (unsigned)e; }, V.Np);
-    }
-#else
     if constexpr (KQ == 0) {
       Ld.template load_lanes<false>(Hr + rowoff, 32, V.Np);
     } else if constexpr (KQ == 2) {
@@ -1336,7 +1228,6 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
       const uint16_t* row = Hr + rowoff;
       Ld.load([&](int e) { return row + (unsigned)e; }, V.Np);
     }
-#endif
   };
   // Line2 loads each line when it starts (no prefetch: 48 VGPRs, the 4th wave per SIMD)
   constexpr bool kPF = KQ != 2;
@@ -1361,13 +1252,7 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
       }
 #endif
       if (kPF && r + 1 < (w + 1) * RPW && i + 1 < V.Mp) load_row(Lnext, i + 1);
-#if defined(ACOSS_FK_ROWS)
-      const LineCells<true> keyf{V, i, reinterpret_cast<const uint32_t*>(Hr) - (size_t)i0 * ldr, ldr};
-#elif defined(ACOSS_LO_PLANE)
-      const LineCells<true> keyf{V, i, Klo + (size_t)p * kstride, ldr};
-#else
       const LineCells<true> keyf{V, i};
-#endif
       float th, T;
       Group c_lo, c_hi;
       c_lo.g = c_hi.g = -1;
@@ -1430,11 +1315,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
   if (i0 >= V.Mp || V.Np <= 0) return;
   // the strip's row-major plane: per pair, or a slot of this XCD's ring (HrRing)
   __shared__ int s_slot;
-#ifdef ACOSS_FK_ROWS
-  uint16_t* Hr = reinterpret_cast<uint16_t*>(reinterpret_cast<uint32_t*>(K.hr) + (size_t)p * kstride + (size_t)i0 * ldr);
-#else
   uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
-#endif
   if (K.ring.slots) {
     if (threadIdx.x == 0) {
       unsigned xcc;
@@ -1464,13 +1345,13 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
   WaveLds* wl = reinterpret_cast<WaveLds*>(smem);
   uint32_t(*rowbits)[RB] = reinterpret_cast<uint32_t(*)[RB]>(smem + 4 * sizeof(WaveLds));
   if (KQ == 8 || (KQ != 16 && V.Np <= short_n))
-    rows_body<4, 8, RB>(V, p, strip, Hr, ldr, K.lo, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+    rows_body<4, 8, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   else if (KQ == 16)  // (mixed launches leave it out: a third select in one kernel costs more than it saves)
-    rows_body<4, 16, RB>(V, p, strip, Hr, ldr, K.lo, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+    rows_body<4, 16, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   else if (KQ == 2 && V.Np > 2048)
-    rows_body<4, 2, RB>(V, p, strip, Hr, ldr, K.lo, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+    rows_body<4, 2, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   else
-    rows_body<4, 0, RB>(V, p, strip, Hr, ldr, K.lo, kstride, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
+    rows_body<4, 0, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   if (K.ring.slots) {  // every wave's reads of the slot have returned: hand it to ticket t + S
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(K.ring.gen + s_slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1562,13 +1443,7 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
     // Line2: the second half's strip 64 + lane
     const size_t w2 = (size_t)p * mask_stride + (size_t)(2048 + lane * KPL < V.Mp ? 64 + lane : 0) * ld + j;
     const uint32_t rt2 = KQ == 2 ? RT[w2] : 0u;
-#if defined(ACOSS_FK_ROWS)
-    const LineCells<false> keyf{V, j, reinterpret_cast<const uint32_t*>(K.hr) + (size_t)p * kstride, ldc};
-#elif defined(ACOSS_LO_PLANE)
-    const LineCells<false> keyf{V, j, K.lo + (size_t)p * kstride, ldc};
-#else
     const LineCells<false> keyf{V, j};
-#endif
     float th, Tc;
     Group c_lo, c_hi;
     c_lo.g = c_hi.g = -1;
@@ -1631,15 +1506,7 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
                      uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s) {
   if (B.m != kMS || B.tau != 1 || L > 4096) return 1;
   const size_t plane = (size_t)nb * kstride;
-#if defined(ACOSS_FK_ROWS)
-  // full-key row-major plane (4 B/cell) first, then the strip-major 16-bit plane
-  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + 2 * plane, HrRing{}, nullptr};
-#elif defined(ACOSS_LO_PLANE)
-  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane, ring,
-                    static_cast<uint16_t*>(kplanes) + 2 * plane};
-#else
-  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane, ring, nullptr};
-#endif
+  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane, ring};
   const int nstrips = (L + kSR - 1) / kSR;
   // launches whose lines all fit 512 / 1024 codes take LineS<8> / LineS<16> throughout; in
   // mixed launches each pair picks per side (lines of <= short_n codes LineS<8>, past 2048
