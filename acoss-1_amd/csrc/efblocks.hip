@@ -25,16 +25,28 @@ namespace {
 
 constexpr int kEfMaxR = 64;    // rows per block feature (reference: 50 and 40)
 constexpr int kEfMaxD = 32;    // MFCC coefficients (reference: 20)
-constexpr int kEfMaxRad = 512; // Gaussian radius (sigma < 128: blocks of < 12,800 frames at R = 50)
+constexpr int kEfMaxRad = 512; // Gaussian taps kept in LDS (sigma < 128: blocks of < 12,800 frames at R = 50)
 
-// filtered value of column c at frame i of the block (zero outside [0, n_in))
+// Gaussian tap t (|t| <= rad) of a radius above kEfMaxRad, formed on the fly exactly as the LDS
+// table would hold it: exp(-x^2 / (2 sigma^2)) divided by the sequential sum of all taps.
+__device__ __forceinline__ double ef_tap(int t, double s2, double wsum) {
+  const double x = (double)t;
+  return exp(-0.5 / s2 * (x * x)) / wsum;
+}
+
+// filtered value of column c at frame i of the block (zero outside [0, n_in)); taps from the LDS
+// table w when rad <= kEfMaxRad, else on the fly (s2 = sigma^2, wsum = the taps' sum)
 __device__ __forceinline__ double ef_filtered(const float* X, int64_t ld, int n_in, int c, int i, const double* w,
-                                              int rad) {
+                                              int rad, double s2, double wsum) {
   if (i < 0 || i >= n_in) return 0.0;
   if (rad == 0) return (double)X[(int64_t)i * ld + c];
   double acc = 0.0;
   const int t0 = max(-rad, -i), t1 = min(rad, n_in - 1 - i);
-  for (int t = t0; t <= t1; ++t) acc = fma(w[t + rad], (double)X[(int64_t)(i + t) * ld + c], acc);
+  if (rad <= kEfMaxRad) {
+    for (int t = t0; t <= t1; ++t) acc = fma(w[t + rad], (double)X[(int64_t)(i + t) * ld + c], acc);
+  } else {
+    for (int t = t0; t <= t1; ++t) acc = fma(ef_tap(t, s2, wsum), (double)X[(int64_t)(i + t) * ld + c], acc);
+  }
   return acc;
 }
 
@@ -44,9 +56,18 @@ __device__ void ef_resize(const float* X, int64_t ld, int n_in, int R, int D, do
   const double sigma = fmax(0.0, (factor - 1.0) / 2.0);
   if (threadIdx.x == 0) *s_rad = sigma > 0.0 ? (int)(4.0 * sigma + 0.5) : 0;
   __syncthreads();
-  const int rad = min(*s_rad, kEfMaxRad);
-  if (rad > 0) {
-    const double s2 = sigma * sigma;
+  const int rad = *s_rad;
+  const double s2 = sigma * sigma;
+  double wsum = 0.0;
+  if (rad > kEfMaxRad) {  // very long beat blocks: the taps' sum here, the taps in ef_filtered
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+      for (int t = -rad; t <= rad; ++t) s += exp(-0.5 / s2 * ((double)t * (double)t));
+      w[0] = s;
+    }
+    __syncthreads();
+    wsum = w[0];
+  } else if (rad > 0) {
     for (int t = threadIdx.x; t <= 2 * rad; t += blockDim.x) {
       const double x = (double)(t - rad);
       w[t] = exp(-0.5 / s2 * (x * x));
@@ -68,8 +89,8 @@ __device__ void ef_resize(const float* X, int64_t ld, int n_in, int R, int D, do
     const double fl = floor(cc);
     const int i0 = (int)fl;
     const double f = cc - fl;
-    const double v0 = ef_filtered(X, ld, n_in, c, i0, w, rad);
-    const double v1 = ef_filtered(X, ld, n_in, c, i0 + 1, w, rad);
+    const double v0 = ef_filtered(X, ld, n_in, c, i0, w, rad, s2, wsum);
+    const double v1 = ef_filtered(X, ld, n_in, c, i0 + 1, w, rad, s2, wsum);
     double v = (1.0 - f) * v0 + f * v1;
     if (!(v == v) || v == INFINITY || v == -INFINITY) v = 0.0;  // ret[isinf|isnan] = 0 (:244-245)
     out[e] = v;

@@ -160,7 +160,8 @@ def test_ef_block_features_gpu_vs_restatement():
     from acoss import _lib
     rng = np.random.default_rng(12)
     chromas, mfccs, onsets = [], [], []
-    for n, period in [(900, 43), (2601, 37), (500, 11), (4001, 60), (860, 43)]:
+    # (16000, 700): beat blocks of ~14,000 frames, Gaussian radii past the LDS tap table (on-the-fly taps)
+    for n, period in [(900, 43), (2601, 37), (500, 11), (4001, 60), (860, 43), (16000, 700)]:
         chromas.append(np.abs(rng.normal(size=(n, 12))).astype(np.float32))
         m = rng.normal(size=(20, n)).astype(np.float32)
         m[1, 5] = np.nan
