@@ -535,10 +535,6 @@ def ef_block_features(chromas, mfccs, onsets, blocksize=20, mfccs_per_block=50, 
         if nb[t]:
             if o.min() < 0 or o.max() > n[t] or np.any(np.diff(o) <= 0):
                 raise ValueError("track %d: onsets must increase inside the track" % t)
-            span = o[blocksize:] - o[:-blocksize]
-            if span.max() > 256 * min(mfccs_per_block, chromas_per_block):
-                raise ValueError("track %d: a beat block spans more than %d frames" %
-                                 (t, 256 * min(mfccs_per_block, chromas_per_block)))
     foff = np.zeros(T, np.int64)
     foff[1:] = np.cumsum(n[:-1])
     ooff = np.zeros(T, np.int64)

@@ -151,7 +151,7 @@ def _fusion_ws(Ws, K=5, niters=20, reg_diag=1):
     for Jt in Js:
         _lib.check_knn(Jt, Pts[0].shape[0])
     world, rank = _shard_world()
-    if world > 1:
+    if world > 1 and Pts[0].shape[0] >= world:  # (fewer rows than ranks: every rank runs it whole)
         return _fusion_sharded(Pts, Js, Vs, niters, reg_diag, world, rank)
     for it in range(niters):
         # the reference's `Pts = nextPts` aliasing: from the second iteration on, matrix i's
@@ -180,9 +180,9 @@ def _shard_world():
 
 
 def shard_rows(n, world):
-    """[(r0, r1)] per rank: equal row stripes (every row of a step costs the same, K gathered rows)."""
-    per = -(-n // world)
-    return [(min(n, r * per), min(n, (r + 1) * per)) for r in range(world)]
+    """[(r0, r1)] per rank: row stripes within one row of each other (every row of a step costs the
+    same, K gathered rows); none is empty when n >= world."""
+    return [(r * n // world, (r + 1) * n // world) for r in range(world)]
 
 
 def _fusion_sharded(Pts, Js, Vs, niters, reg_diag, world, rank):
@@ -197,8 +197,6 @@ def _fusion_sharded(Pts, Js, Vs, niters, reg_diag, world, rank):
     n = Pts[0].shape[0]
     bounds = shard_rows(n, world)
     r0, r1 = bounds[rank]
-    if r1 <= r0:
-        raise ValueError("SNF row sharding needs at least one row per rank (n=%d, world=%d)" % (n, world))
     St = [P[r0:r1].contiguous() for P in Pts]
     N = len(St)
     for it in range(niters):

@@ -131,6 +131,7 @@ def other_paths(nth, seed):
       earlyfusion: EarlyFusion.similarity (earlyfusion_traile.py:157-198) batched over every pair of
         80 tracks x 446 beat blocks (synthetic block features); flops/pair = 2*(1000+1225+480)*M*N
         on the fp32 MFMA CSMs, plus 4 SW and 3 WCSMs.
+      snf: one SNF cross-diffusion step at Da-TACOS size (snf_path).
     """
     import torch
     import oracle
@@ -225,7 +226,59 @@ def other_paths(nth, seed):
                           "cpu_baseline": {"value": round(ncpu / cdt, 3), "cores": 1, "kind": "port",
                                            "sample": "%d pairs, numpy restatement + C SW oracle, %.1f s" % (ncpu, cdt)},
                           "scores_equal_to_oracle": "%d of %d" % (agree, 4 * ncpu)}
+    # ---- SNF cross-diffusion step (f2) at Da-TACOS size
+    res["snf"] = snf_path(seed)
     return res
+
+
+def snf_path(seed, n=15000, L=2, K=20, n_cpu=2000):
+    """One SNF cross-diffusion step (acoss_snf_step, similarity_fusion.py:163-174) on n x n float64
+    matrices, n = 15,000 (Da-TACOS), L = 2 (ChenFusion), K = 20; HBM-bound: algorithmic bytes
+    (L + 4) * 8 n^2 per step. The CPU sample is the reference's own scipy expression
+    (np_oracle.snf_step, one core) at n = n_cpu, with the GPU step at that size checked against it."""
+    import torch
+    from acoss import _lib
+    from oracle import np_oracle as npo
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    mats = [torch.rand((n, n), dtype=torch.float64, device="cuda", generator=g) for _ in range(L)]
+    W = torch.rand((n, n), dtype=torch.float32, device="cuda", generator=g)
+    V, J = torch.topk(W, K, dim=1)
+    del W
+    V = (V / V.sum(1, keepdim=True)).to(torch.float64)
+    J = J.to(torch.int32)
+    out = torch.empty((n, n), dtype=torch.float64, device="cuda")
+    _lib.snf_step(mats, 0, J, V, 1.0, out=out)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for r in range(5):
+        ev0.record(s)
+        _lib.snf_step(mats, r % L, J, V, 1.0, out=out, validated=True)
+        ev1.record(s)
+        ev1.synchronize()
+        ts.append(ev0.elapsed_time(ev1))
+    ms = float(np.median(ts))
+    del mats, out
+    torch.cuda.empty_cache()
+    algo = (L + 4) * 8.0 * n * n
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cm = [rng.random((n_cpu, n_cpu)) for _ in range(L)]
+    cJ = np.stack([rng.choice(n_cpu, K, replace=False) for _ in range(n_cpu)]).astype(np.int32)
+    cV = rng.random((n_cpu, K))
+    cV /= cV.sum(1, keepdims=True)
+    t0 = time.perf_counter()
+    ref = npo.snf_step(cm, 0, cJ, cV, 1.0)
+    cdt = time.perf_counter() - t0
+    got = _lib.snf_step([torch.as_tensor(m).cuda() for m in cm], 0, cJ, cV, 1.0).cpu().numpy()
+    return {"metric": "SNF cross-diffusion steps/s (n = %d, L = %d, K = %d)" % (n, L, K),
+            "value": round(1e3 / ms, 2), "ms": round(ms, 3), "dtype": "f64",
+            "roofline": {"bound": "hbm", "achieved": round(algo / (ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(algo / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                         "bytes_per_step": algo},
+            "cpu_baseline": {"value": round(1.0 / cdt, 3), "cores": 1, "kind": "port",
+                             "sample": "one step at n = %d (scipy csr, np_oracle.snf_step), %.2f s" % (n_cpu, cdt)},
+            "bitexact_vs_scipy_n%d" % n_cpu: bool(np.array_equal(got, ref))}
 
 
 def host_info():

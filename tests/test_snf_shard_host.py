@@ -95,8 +95,9 @@ def test_sharded_fusion_equals_world1(tmp_path, monkeypatch, world, n, L):
 
 def test_shard_rows_cover():
     from acoss.algorithms.utils.similarity_fusion import shard_rows
-    for n, w in [(10, 3), (15000, 8), (7, 7), (9, 2)]:
+    for n, w in [(10, 3), (15000, 8), (7, 7), (9, 2), (9, 8)]:
         b = shard_rows(n, w)
         assert b[0][0] == 0 and b[-1][1] == n and len(b) == w
         assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
-        assert max(r1 - r0 for r0, r1 in b) - min(r1 - r0 for r0, r1 in b) <= -(-n // w)
+        assert max(r1 - r0 for r0, r1 in b) - min(r1 - r0 for r0, r1 in b) <= 1
+        assert all(r1 > r0 for r0, r1 in b)
