@@ -1,0 +1,57 @@
+"""Batched EarlyFusion scoring (acoss_earlyfusion) on the bench's synthetic bank: 80 tracks x 446
+beat blocks (mfcc 1000-d, ssm 1225-d, chroma 480-d block features), every unordered pair.
+
+    python tools/ef_bench.py [--tracks 80] [--blocks 446] [--reps 3]
+
+Prints pairs/s per repetition (HIP events on the launch stream) and a checksum of the scores, so
+library variants (ACOSS_HIP_LIB=...) can be compared and checked against each other; rocprofv3
+gives the per-kernel split.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "acoss-1_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from acoss import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tracks", type=int, default=80)
+    ap.add_argument("--blocks", type=int, default=446)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=20250101)
+    a = ap.parse_args()
+    rng = np.random.Generator(np.random.PCG64(a.seed))
+    NT, NB = a.tracks, a.blocks
+    mf = rng.standard_normal((NT * NB, 1000), dtype=np.float32)
+    ss = np.abs(rng.standard_normal((NT * NB, 1225), dtype=np.float32))
+    ch = np.abs(rng.standard_normal((NT * NB, 480), dtype=np.float32))
+    med = np.abs(rng.standard_normal((NT, 12), dtype=np.float32))
+    bank = {"mfccs": torch.as_tensor(mf).cuda(), "ssms": torch.as_tensor(ss).cuda(),
+            "chromas": torch.as_tensor(ch).cuda(), "chroma_med": torch.as_tensor(med).cuda(),
+            "off": torch.as_tensor(np.arange(NT, dtype=np.int64) * NB).cuda(),
+            "nb": torch.as_tensor(np.full(NT, NB, np.int32)).cuda(), "max_blocks": NB}
+    pairs = np.array([(i, j) for i in range(NT) for j in range(i + 1, NT)], np.int32)
+    _lib.earlyfusion(bank, pairs[:64], 0.1, 10)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for r in range(a.reps):
+        e0.record(s)
+        sc = _lib.earlyfusion(bank, pairs, 0.1, 10)
+        e1.record(s)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        print("rep %d: %.1f pairs/s (%.2f ms)" % (r, len(pairs) / (ms * 1e-3), ms))
+    v = sc.double().cpu().numpy()
+    print("score checksum %.6f" % float(np.sum(v * np.arange(1, v.size + 1).reshape(v.shape) % 7919)))
+
+
+if __name__ == "__main__":
+    main()
