@@ -178,6 +178,126 @@ __global__ __launch_bounds__(256) void k_ef_csm(const float* __restrict__ bank, 
   }
 }
 
+typedef float f32x4e __attribute__((ext_vector_type(4)));
+
+// Row-padded copy of a feature bank (nrows x d -> nrows x ldp, zeros in [d, ldp)) so that
+// k_ef_csm_w's 16-byte row loads are aligned for any d (the SSM blocks have d = 1225). The zero
+// columns add exact +0 terms at the end of every fmaf chain, so the CSM is unchanged bit for bit.
+__global__ void k_ef_pad_rows(const float* __restrict__ X, int64_t nrows, int d, int ldp, float* __restrict__ Xp) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= nrows) return;
+  for (int c = threadIdx.x & 63; c < ldp; c += 64) Xp[row * ldp + c] = c < d ? X[row * d + c] : 0.0f;
+}
+
+// Euclidean CSM tiles with no LDS and no barriers: one WAVE per 64 x 64 output tile (2 x 2
+// accumulators of 32x32x2 f32 MFMAs), operands loaded straight into registers. Per block of KB
+// k-values, lane l (r = l % 32, h = l / 32) reads KB / 2 contiguous floats of each of its four
+// operand rows (k0 + h KB / 2 ..., 16-byte loads: the two halves cover KB floats of the row),
+// and one v_permlane32_swap per register pair turns that into the MFMA layout (step s: half h
+// holds k0 + 2 s + h), so every output is the same ascending-k fmaf chain as k_ef_csm:
+// bit-identical. The loads run DEPTH - 1 blocks ahead of the multiplies (a ring of register
+// blocks; the last blocks' look-ahead loads are clamped to a valid block and never used).
+// Needs d % 4 == 0 (16-byte aligned rows; acoss_earlyfusion pads the SSM bank).
+#ifndef ACOSS_EF_KB
+#define ACOSS_EF_KB 16
+#endif
+#ifndef ACOSS_EF_DEPTH
+#define ACOSS_EF_DEPTH 3
+#endif
+#ifndef ACOSS_EF_WPE
+#define ACOSS_EF_WPE 2
+#endif
+__global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w(const float* __restrict__ bank, int d,
+                                                                const float* __restrict__ sq, EfPairs E, int ld,
+                                                                int n_tiles, float* __restrict__ out) {
+  constexpr int KB = ACOSS_EF_KB, DEPTH = ACOSS_EF_DEPTH, NQ = KB / 8;  // NQ 16-byte loads per row
+  const int tiles = (ld + kT - 1) / kT;
+  const int lb = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int tile = lb * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (tile >= n_tiles) return;
+  const int p = tile / (tiles * tiles), tix = tile - p * tiles * tiles;
+  int a, b, M, N;
+  pair_dims(E, p, &a, &b, &M, &N);
+  const int bi = (tix / tiles) * kT, bj = (tix % tiles) * kT;
+  if (bi >= M || bj >= N) return;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  // this lane's four operand rows (clamped into the track: rows past M / N are never stored)
+  const float* rows[4] = {bank + (E.off[a] + min(bi + r, M - 1)) * (int64_t)d + (KB / 2) * h,
+                          bank + (E.off[a] + min(bi + 32 + r, M - 1)) * (int64_t)d + (KB / 2) * h,
+                          bank + (E.off[b] + min(bj + r, N - 1)) * (int64_t)d + (KB / 2) * h,
+                          bank + (E.off[b] + min(bj + 32 + r, N - 1)) * (int64_t)d + (KB / 2) * h};
+  const int nfull = d / KB;
+  f32x4e ring[DEPTH][4][NQ];
+  auto load = [&](f32x4e (&v)[4][NQ], int blk) {  // a whole block (clamped to the last whole one)
+    const int k0 = min(blk, nfull - 1) * KB;
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) v[o][q] = *reinterpret_cast<const f32x4e*>(rows[o] + k0 + 4 * q);
+  };
+  f32x16 acc[2][2] = {};
+  // operands of steps s and s + KB / 4 come from registers 2 s and 2 s + 1 of every operand row
+  auto mul = [&](const f32x4e (&v)[4][NQ]) {
+    float op[4][KB / 2];
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int s2 = 0; s2 < KB / 4; ++s2) {
+        const float lo = v[o][s2 >> 1][(s2 & 1) * 2], hi = v[o][s2 >> 1][(s2 & 1) * 2 + 1];
+        const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, lo),
+                                                         __builtin_bit_cast(unsigned, hi), false, false);
+        op[o][s2] = __builtin_bit_cast(float, (unsigned)sw[0]);
+        op[o][s2 + KB / 4] = __builtin_bit_cast(float, (unsigned)sw[1]);
+      }
+#pragma unroll
+    for (int st = 0; st < KB / 2; ++st) {
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[0][st], op[2][st], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[0][st], op[3][st], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[1][st], op[2][st], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[1][st], op[3][st], acc[1][1], 0, 0, 0);
+    }
+  };
+  if (nfull > 0) {
+#pragma unroll
+    for (int i = 0; i < DEPTH - 1; ++i) load(ring[i], i);
+#pragma unroll 1
+    for (int kb = 0; kb < nfull; kb += DEPTH) {
+#pragma unroll
+      for (int j = 0; j < DEPTH; ++j) {
+        load(ring[(j + DEPTH - 1) % DEPTH], kb + j + DEPTH - 1);
+        __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the multiplies they overlap
+        if (kb + j < nfull) mul(ring[j]);
+      }
+    }
+  }
+  if (d % KB) {  // the partial tail block: zeros past d
+    const int k0 = nfull * KB;
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        ring[0][o][q] = k0 + (KB / 2) * h + 4 * q < d ? *reinterpret_cast<const f32x4e*>(rows[o] + k0 + 4 * q)
+                                                       : f32x4e{0.0f, 0.0f, 0.0f, 0.0f};
+    mul(ring[0]);
+  }
+  float* ob = out + (size_t)p * ld * ld;
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj) {
+      const int col = bj + 32 * tj + r;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = bi + 32 * ti + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (row < M && col < N) {
+          float c2 = (sq[E.off[a] + row] + sq[E.off[b] + col]) - 2.0f * acc[ti][tj][reg];
+          if (c2 < 0.0f) c2 = 0.0f;
+          ob[(size_t)row * ld + col] = sqrtf(c2);
+        }
+      }
+    }
+}
+
 // The nn smallest of every row -> 1, ties lowest column (csm_to_binary). A block of 16 waves
 // takes 16 rows (one wave per row) and writes them as one row of u16 bit words (bit r = row
 // 16g + r) in LDS, then to the pair's bit plane for SW. blockIdx.z = CSM plane, written to
@@ -486,6 +606,16 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   ACOSS_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_ef_rows, dim3(rb), dim3(256), 0, s, chroma, nrows, d_chroma, 1, chn, nullptr);
   ACOSS_LAUNCH_CHECK();
+  static const bool wave_tiles = getenv("ACOSS_EF_LDS_CSM") == nullptr;
+  const float* ssm_p = nullptr;  // SSM bank with rows padded to a multiple of 4 (k_ef_csm_w)
+  if (wave_tiles && d_ssm % 4 != 0) {
+    const int ldp = (int)align_up((size_t)d_ssm, 4);
+    float* pb = static_cast<float*>(workspace(15, (size_t)nrows * ldp * 4));
+    if (!pb) return ACOSS_E_HIP;
+    hipLaunchKernelGGL(k_ef_pad_rows, dim3(rb), dim3(256), 0, s, ssm, nrows, d_ssm, ldp, pb);
+    ACOSS_LAUNCH_CHECK();
+    ssm_p = pb;
+  }
   prof_end(PH_CSM, s);
 
   // chunk of pairs: 3 CSMs (E overwrites the first), 4 binary matrices, 6 mean vectors, SW scratch
@@ -525,11 +655,24 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
     prof_begin(PH_CSM, s);
     hipLaunchKernelGGL(k_ef_oti, dim3((P + 255) / 256), dim3(256), 0, s, chroma_med, pairs + 2 * p0, P, oti);
     ACOSS_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ef_csm<0>, dim3((unsigned)(tiles * tiles * P)), dim3(256), 0, s, mfcc, d_mfcc, sq_m, E, oti, ld, C);
-    ACOSS_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ef_csm<0>, dim3((unsigned)(tiles * tiles * P)), dim3(256), 0, s, ssm, d_ssm, sq_s, E, oti, ld,
-                       C + mstride);
-    ACOSS_LAUNCH_CHECK();
+    {
+      const int n_tiles = tiles * tiles * P;
+      auto euclid = [&](const float* bank, int d, const float* sq, float* dst) -> int {
+        if (wave_tiles && d % 4 != 0 && bank == ssm && ssm_p) {
+          bank = ssm_p;  // the row-padded copy made above
+          d = (int)align_up((size_t)d, 4);
+        }
+        if (wave_tiles && d % 4 == 0)
+          hipLaunchKernelGGL(k_ef_csm_w, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, s, bank, d, sq, E, ld,
+                             n_tiles, dst);
+        else
+          hipLaunchKernelGGL(k_ef_csm<0>, dim3((unsigned)n_tiles), dim3(256), 0, s, bank, d, sq, E, oti, ld, dst);
+        ACOSS_LAUNCH_CHECK();
+        return ACOSS_OK;
+      };
+      if (euclid(mfcc, d_mfcc, sq_m, C) != ACOSS_OK || euclid(ssm, d_ssm, sq_s, C + mstride) != ACOSS_OK)
+        return ACOSS_E_HIP;
+    }
     hipLaunchKernelGGL(k_ef_csm<1>, dim3((unsigned)(tiles * tiles * P)), dim3(256), 0, s, chn, d_chroma, nullptr, E, oti, ld,
                        C + 2 * mstride);
     ACOSS_LAUNCH_CHECK();
