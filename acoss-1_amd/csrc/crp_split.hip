@@ -30,6 +30,7 @@ namespace acoss {
 namespace {
 
 constexpr int kMS = 9;
+
 // 16-bit prefix of "no element": above every real prefix (finite keys >= +0 have prefixes <= 0x7f80)
 constexpr unsigned kNone = 0x7fffu;
 
@@ -1299,8 +1300,8 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
 // full keys back while they are cache-resident (no second pass over F from HBM, one launch
 // fewer). LDS of the two phases is one union.
 // KQ = 8: every line of the launch is short; KQ = 0: each pair picks its row line type (rows of
-// at most short_n codes take LineS<8>; short_n = 0 disables); KQ = 2: as 0, and rows past 2048
-// codes take Line2.
+// at most short_n codes take LineS<8>; short_n = 0 disables); KQ = 16: as 0 with LineS<16> for
+// the rest (every line <= 1024 codes); KQ = 2: as 0, and rows past 2048 codes take Line2.
 template <int KQ>
 __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
                                                           int64_t kstride, float kappa, float* __restrict__ thr,
@@ -1344,9 +1345,12 @@ __global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlan
 #endif
   WaveLds* wl = reinterpret_cast<WaveLds*>(smem);
   uint32_t(*rowbits)[RB] = reinterpret_cast<uint32_t(*)[RB]>(smem + 4 * sizeof(WaveLds));
-  if (KQ == 8 || (KQ != 16 && V.Np <= short_n))
+  // lines of <= short_n codes take LineS<8> in every launch type but KQ = 8 (all short); KQ = 16
+  // launches (every line <= 1024 codes) take LineS<16> for the rest (a third select type in a
+  // KQ = 0 launch costs more than it saves)
+  if (KQ == 8 || V.Np <= short_n)
     rows_body<4, 8, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
-  else if (KQ == 16)  // (mixed launches leave it out: a third select in one kernel costs more than it saves)
+  else if (KQ == 16)
     rows_body<4, 16, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   else if (KQ == 2 && V.Np > 2048)
     rows_body<4, 2, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
@@ -1469,7 +1473,7 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
 
 // KQ = 8: every line of the launch is short (runs of kCPW<8> columns); KQ = 0: runs of kCPW<0>,
 // each pair picking its column line type (columns of at most short_n codes take LineS<8>);
-// KQ = 2: as 0, and columns past 2048 codes take Line2.
+// KQ = 16: as 0 with LineS<16> for the rest; KQ = 2: as 0, and columns past 2048 codes take Line2.
 template <int KQ>
 __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
                                                    const uint32_t* __restrict__ RT, float* __restrict__ thr,
@@ -1484,7 +1488,7 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
   const int j0 = (lb - p * gridDim.x) * kColsPerBlock<KQ> + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCPW<KQ>;
   const int jend = min(j0 + kCPW<KQ>, V.Np);
   WaveLds& W = wl[threadIdx.x >> 6];
-  if (KQ == 8 || (KQ != 16 && V.Mp <= short_n))
+  if (KQ == 8 || V.Mp <= short_n)
     cols_body<8>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
   else if (KQ == 16)
     cols_body<16>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
