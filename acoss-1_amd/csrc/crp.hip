@@ -681,6 +681,89 @@ __global__ __launch_bounds__(64) void k_crp_dp_fast(
 }
 
 // --------------------------------------------------------------------------------------
+// k_crp_dp_grp: the FAST DP (serra09, gamma_open == gamma_ext = K/2) with SEVERAL pairs per
+// wave for CRPs of at most 2048 rows: a group of LP = ceil(L / 32) lanes per pair (lane ll owns
+// rows 32 ll .. 32 ll + 31, one band), G = 64 / LP groups per wave. A one-pair wave walks
+// N' + 63 steps however short the pair; a group walks N' + LP - 1, and every lane keeps 32 rows
+// per step, so short tracks (Da-TACOS lengths: L ~ 500) no longer leave most lanes idle or pay
+// the per-step shuffles for 8 rows. Same recurrence, same DpLane step: bit-identical scores.
+// --------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_crp_dp_grp(const uint32_t* __restrict__ maskT, int64_t mask_stride, int ld,
+                                                   const int2* __restrict__ dims, int nb, int LP, float go,
+                                                   float* __restrict__ out) {
+  constexpr int R = 32;
+  __shared__ float s_best[64];
+  const int lane = threadIdx.x;
+  const int G = 64 / LP;
+  const int g = lane / LP, ll = lane - g * LP;
+  const int p = blockIdx.x * G + g;
+  const bool in_group = g < G && p < nb;
+  const int2 dm = in_group ? dims[p] : make_int2(0, 0);
+  const int Mp = dm.x, Np = dm.y;
+  const int row0 = ll * R;
+  const uint32_t* mrow = maskT + (size_t)(in_group ? p : 0) * mask_stride + (size_t)ll * ld;
+  DpLane<0, true, R, true> L;
+  L.go = go;
+  L.ge = go;
+  L.Np = Np;
+  L.lane = ll;
+  uint32_t rv = 0;
+  for (int r = 0; r < R; ++r) rv |= (uint32_t)((row0 + r >= 2) && (row0 + r < Mp)) << r;
+  L.rowvalid = rv;
+  L.w1 = L.w2 = 0;
+  L.h1 = L.h2 = DpAbove{0.0f, 0.0f, 0u};
+  L.best = 0.0f;
+  float qa[R], qb[R], qc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) qa[r] = qb[r] = qc[r] = 0.0f;
+  DpAbove pub{0.0f, 0.0f, 0u};
+  // steps until every group of the wave is done (wave-uniform bound)
+  const int S_end = (int)wave_max_u32(in_group ? (unsigned)(Np + LP - 1) : 0u);
+  const bool lane_active = in_group && row0 < Mp;
+  auto fetch = [&](int c) -> uint32_t {
+    if (!(lane_active && c >= 2 && c < Np)) return 0u;
+    return mrow[c] & rv;
+  };
+  auto recv = [&](const DpAbove& mine) -> DpAbove {
+    DpAbove h;
+    h.q30 = __shfl_up(mine.q30, 1);
+    h.q31 = __shfl_up(mine.q31, 1);
+    h.b = (uint32_t)__shfl_up((int)mine.b, 1);
+    if (ll == 0) h = DpAbove{0.0f, 0.0f, 0u};  // the group's first rows: nothing above
+    return h;
+  };
+  uint32_t wnext = fetch(-ll);
+  for (int s = 0; s < S_end; s += 3) {
+    {
+      const int c = s - ll;
+      const uint32_t w0 = wnext;
+      wnext = fetch(c + 1);
+      pub = L.step(qa, qb, qc, w0, recv(pub), c);
+    }
+    if (s + 1 < S_end) {
+      const int c = s + 1 - ll;
+      const uint32_t w0 = wnext;
+      wnext = fetch(c + 1);
+      pub = L.step(qc, qa, qb, w0, recv(pub), c);
+    }
+    if (s + 2 < S_end) {
+      const int c = s + 2 - ll;
+      const uint32_t w0 = wnext;
+      wnext = fetch(c + 1);
+      pub = L.step(qb, qc, qa, w0, recv(pub), c);
+    }
+  }
+  // per-group maximum through LDS (groups need not be a power of two wide)
+  s_best[lane] = L.best;
+  __syncthreads();
+  if (in_group && ll == 0) {
+    float b = 0.0f;
+    for (int k = 0; k < LP; ++k) b = fmaxf(b, s_best[lane + k]);
+    out[p] = b;
+  }
+}
+
+// --------------------------------------------------------------------------------------
 // k_crp_dp_pk<ALIGN>: k_crp_dp<ALIGN, true, 32> in packed 16-bit integers. With
 // gamma_open == gamma_ext = K/2 (K a small integer, 1 for the reference's 0.5), every score is
 // a multiple of 1/2, so 2Q is an exact integer below 4 L: lane l keeps rows (h, h + 16) of a
@@ -925,10 +1008,17 @@ int prepare_stage(int m, int ld, Stage* st) {
 
 template <int ALIGN, int R>
 void launch_dp_r(bool eqg, int nb, const uint32_t* maskT, int64_t mstride, int ld, const int2* dims, float go,
-                 float ge, float4* bnd, int64_t bstride, float* out, hipStream_t s) {
+                 float ge, float4* bnd, int64_t bstride, float* out, hipStream_t s, int L = 0) {
   const float k2 = 2.0f * go;
   static const bool no_fast = getenv("ACOSS_DP_NOFAST") != nullptr;
-  if (ALIGN == 0 && eqg && !no_fast && k2 >= 0.0f && k2 <= 1024.0f && k2 == floorf(k2))
+  static const bool no_grp = getenv("ACOSS_DP_NOGROUP") != nullptr;
+  const int LP = (L + 31) / 32;  // lanes per pair at 32 rows per lane
+  if (ALIGN == 0 && eqg && !no_fast && !no_grp && k2 >= 0.0f && k2 <= 1024.0f && k2 == floorf(k2) && L > 0 &&
+      LP <= 21) {  // three or more pairs per wave (two per wave measured slower at L ~ 1000)
+    const int G = 64 / LP;
+    hipLaunchKernelGGL(k_crp_dp_grp, dim3((unsigned)((nb + G - 1) / G)), dim3(64), 0, s, maskT, mstride, ld, dims, nb,
+                       LP, go, out);
+  } else if (ALIGN == 0 && eqg && !no_fast && k2 >= 0.0f && k2 <= 1024.0f && k2 == floorf(k2))
     hipLaunchKernelGGL((k_crp_dp_fast<R>), dim3(nb), dim3(64), 0, s, maskT, mstride, ld, dims, go, ge,
                        bnd, bstride, out);
   else if (eqg)
@@ -953,9 +1043,9 @@ template <int ALIGN>
 void launch_dp(bool eqg, int nb, int L, const uint32_t* maskT, int64_t mstride, int ld, const int2* dims, float go,
                float ge, float4* bnd, int64_t bstride, float* out, hipStream_t s) {
   if (L <= 512)
-    launch_dp_r<ALIGN, 8>(eqg, nb, maskT, mstride, ld, dims, go, ge, bnd, bstride, out, s);
+    launch_dp_r<ALIGN, 8>(eqg, nb, maskT, mstride, ld, dims, go, ge, bnd, bstride, out, s, L);
   else if (L <= 1024)
-    launch_dp_r<ALIGN, 16>(eqg, nb, maskT, mstride, ld, dims, go, ge, bnd, bstride, out, s);
+    launch_dp_r<ALIGN, 16>(eqg, nb, maskT, mstride, ld, dims, go, ge, bnd, bstride, out, s, L);
   else if (ALIGN == 1 && dp_packed_ok(eqg, L, go))
     hipLaunchKernelGGL(k_crp_dp_pk<ALIGN>, dim3(nb), dim3(64), 0, s, maskT, mstride, ld, dims, (unsigned)(2.0f * go), bnd,
                        bstride, out);
