@@ -144,11 +144,14 @@ def test_crp_align_run_edges():
 
 
 @pytest.mark.parametrize("lengths", [[10, 41, 42, 73, 74, 137, 300, 521],   # lines <= 512: lane-strided selects
-                                     [300, 522, 600, 777, 1000, 1033]])  # just past 512: the long-line path
+                                     [300, 522, 600, 777, 1000, 1033],  # just past 512: the long-line path
+                                     [100, 250, 400, 460, 505],  # DP: 4 pairs per wave (k_crp_dp_grp)
+                                     [530, 560, 610, 640, 681]])  # DP: 3 pairs per wave, 20 pairs (not a multiple)
 def test_crp_align_short_lines(lengths):
     """Lane-strided selects for batches whose lines all fit 512 codes (element l + 64 q on lane
     l): line ends at every 64-element boundary, a full last lane, silences; and the switch back
-    to the long-line path one code later."""
+    to the long-line path one code later. The short batches also run the grouped Qmax DP
+    (several pairs per wave, ragged N' inside a wave, a partly filled last wave)."""
     rng = np.random.Generator(np.random.PCG64(sum(lengths)))
     tracks = []
     for n in lengths:
