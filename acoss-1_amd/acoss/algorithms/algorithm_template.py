@@ -87,11 +87,22 @@ class CoverAlgorithm(object):
     def load_features(self, i):
         """Feature dict of song i; records its clique as a side effect (:70-94)."""
         feats = _load_feature_file(self.filepaths[i])
-        label = feats["label"]
+        self._record_clique(i, feats["label"])
+        return feats
+
+    def _record_clique(self, i, label):
         if label not in self.cliques:
             self.cliques[label] = set([])
         self.cliques[label].add(i)
-        return feats
+
+    def load_features_many(self, keys):
+        """The `keys` entries (plus 'label') of every song's feature file, read on a thread pool,
+        in song order; records the cliques as load_features does."""
+        from ..features_io import load_many
+        out = load_many(self.filepaths, keys=tuple(keys) + ("label",))
+        for i, f in enumerate(out):
+            self._record_clique(i, f["label"])
+        return out
 
     def get_all_clique_ids(self, verbose=False):
         """Clique membership of every song, cached in '<prefix>_clique_info.txt' (:96-119)."""

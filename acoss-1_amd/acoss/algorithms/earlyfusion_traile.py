@@ -92,7 +92,11 @@ class EarlyFusion(CoverAlgorithm):
         """Block features of songs idx in one acoss_ef_block_features launch; cached in memory and
         on disk like load_features."""
         tic = time.time()
-        feats = [CoverAlgorithm.load_features(self, i) for i in idx]
+        from ..features_io import load_many
+        feats = load_many([self.filepaths[i] for i in idx],
+                          keys=(self.chroma_type, "mfcc_htk", "madmom_features", "label"))
+        for i, f in zip(idx, feats):
+            self._record_clique(i, f["label"])
         chroma = [np.asarray(f[self.chroma_type], np.float32) for f in feats]
         mfcc = [np.array(f['mfcc_htk'], dtype=np.float32).T for f in feats]
         onsets = [np.asarray(f['madmom_features']['onsets'], np.int64) for f in feats]

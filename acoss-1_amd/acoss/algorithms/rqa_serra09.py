@@ -51,7 +51,7 @@ class ChromaBackedAlgorithm(CoverAlgorithm):
     def prepare(self):
         if self._prepared:
             return
-        chromas = [CoverAlgorithm.load_features(self, i)[self.chroma_type] for i in range(self.N)]
+        chromas = [f[self.chroma_type] for f in self.load_features_many((self.chroma_type,))]
         out, out_off, out_len = self._downsample(chromas)
         host = out.cpu().numpy()
         for i in range(self.N):

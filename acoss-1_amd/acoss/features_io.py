@@ -74,18 +74,33 @@ def save_h5(path, mats, h5py):
             f.create_dataset(str(k), data=np.asarray(v))
 
 
-def load_features(path):
-    """Feature dict of one track; IOError if no readable file exists."""
+def load_features(path, keys=None):
+    """Feature dict of one track; IOError if no readable file exists. keys: read only these
+    top-level entries (e.g. the chroma type and 'label'); None reads the whole dict."""
     if os.path.exists(path) and not path.endswith(".npz"):
         try:
-            return _load_h5(path)
+            d = _load_h5(path)
+            return d if keys is None else {k: d[k] for k in keys if k in d}
         except ImportError:
             pass
     p = _npz_path(path)
     if os.path.exists(p):
         with np.load(p, allow_pickle=False) as z:
-            return _unflatten({k: z[k] for k in z.files})
+            names = z.files if keys is None else [k for k in z.files if k.split("/")[0] in keys]
+            return _unflatten({k: z[k] for k in names})
     raise IOError("no readable feature file for %s (looked for HDF5 with h5py, and %s)" % (path, p))
+
+
+def load_many(paths, keys=None, workers=None):
+    """load_features over many tracks on a thread pool (file reads and decompression release
+    the GIL), results in input order."""
+    from concurrent.futures import ThreadPoolExecutor
+    if workers is None:
+        workers = min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1)
+    if workers <= 1 or len(paths) <= 1:
+        return [load_features(p, keys) for p in paths]
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        return list(ex.map(lambda p: load_features(p, keys), paths))
 
 
 def save_features(path, feats):
