@@ -207,10 +207,16 @@ __global__ void k_ef_pad_rows(const float* __restrict__ X, int64_t nrows, int d,
 #ifndef ACOSS_EF_WPE
 #define ACOSS_EF_WPE 2
 #endif
+// KIND = 1: the cosine chroma CSM of get_csm_blocked_oti (pre-normalised rows, 1 - dot): blocks
+// of KB = 24 k-values, so each half-wave holds one whole 12-bin chroma block of a row and the
+// query rows' OTI roll (X1[12 g + c] = X[12 g + (c - oti) mod 12], wave-uniform per pair) is a
+// register rotation; needs d % 24 == 0.
+template <int KIND>
 __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w(const float* __restrict__ bank, int d,
-                                                                const float* __restrict__ sq, EfPairs E, int ld,
+                                                                const float* __restrict__ sq, EfPairs E,
+                                                                const int* __restrict__ oti, int ld,
                                                                 int n_tiles, float* __restrict__ out) {
-  constexpr int KB = ACOSS_EF_KB, DEPTH = ACOSS_EF_DEPTH, NQ = KB / 8;  // NQ 16-byte loads per row
+  constexpr int KB = KIND == 1 ? 24 : ACOSS_EF_KB, DEPTH = ACOSS_EF_DEPTH, NQ = KB / 8;  // NQ 16-byte loads per row
   const int tiles = (ld + kT - 1) / kT;
   const int lb = xcd_remap((int)blockIdx.x, (int)gridDim.x);
   const int tile = lb * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -236,8 +242,32 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w(const float* __r
       for (int q = 0; q < NQ; ++q) v[o][q] = *reinterpret_cast<const f32x4e*>(rows[o] + k0 + 4 * q);
   };
   f32x16 acc[2][2] = {};
+  const int roll = KIND == 1 ? __builtin_amdgcn_readfirstlane(oti[p]) : 0;
   // operands of steps s and s + KB / 4 come from registers 2 s and 2 s + 1 of every operand row
-  auto mul = [&](const f32x4e (&v)[4][NQ]) {
+  auto mul = [&](const f32x4e (&vin)[4][NQ]) {
+    f32x4e v[4][NQ];
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) v[o][q] = vin[o][q];
+    if constexpr (KIND == 1) {  // rotate the query rows' 12-bin block by the pair's OTI
+      if (roll) {
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+          float e[12], t[12];
+#pragma unroll
+          for (int c = 0; c < 12; ++c) e[c] = vin[o][c >> 2][c & 3];
+#pragma unroll
+          for (int R = 1; R < 12; ++R)
+            if (roll == R) {
+#pragma unroll
+              for (int c = 0; c < 12; ++c) t[c] = e[(c - R + 12) % 12];
+            }
+#pragma unroll
+          for (int c = 0; c < 12; ++c) v[o][c >> 2][c & 3] = t[c];
+        }
+      }
+    }
     float op[4][KB / 2];
 #pragma unroll
     for (int o = 0; o < 4; ++o)
@@ -290,9 +320,13 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w(const float* __r
       for (int reg = 0; reg < 16; ++reg) {
         const int row = bi + 32 * ti + (reg & 3) + 8 * (reg >> 2) + 4 * h;
         if (row < M && col < N) {
-          float c2 = (sq[E.off[a] + row] + sq[E.off[b] + col]) - 2.0f * acc[ti][tj][reg];
-          if (c2 < 0.0f) c2 = 0.0f;
-          ob[(size_t)row * ld + col] = sqrtf(c2);
+          if constexpr (KIND == 1) {
+            ob[(size_t)row * ld + col] = 1.0f - acc[ti][tj][reg];
+          } else {
+            float c2 = (sq[E.off[a] + row] + sq[E.off[b] + col]) - 2.0f * acc[ti][tj][reg];
+            if (c2 < 0.0f) c2 = 0.0f;
+            ob[(size_t)row * ld + col] = sqrtf(c2);
+          }
         }
       }
     }
@@ -663,8 +697,8 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
           d = (int)align_up((size_t)d, 4);
         }
         if (wave_tiles && d % 4 == 0)
-          hipLaunchKernelGGL(k_ef_csm_w, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, s, bank, d, sq, E, ld,
-                             n_tiles, dst);
+          hipLaunchKernelGGL(k_ef_csm_w<0>, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, s, bank, d, sq, E,
+                             oti, ld, n_tiles, dst);
         else
           hipLaunchKernelGGL(k_ef_csm<0>, dim3((unsigned)n_tiles), dim3(256), 0, s, bank, d, sq, E, oti, ld, dst);
         ACOSS_LAUNCH_CHECK();
@@ -673,8 +707,12 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
       if (euclid(mfcc, d_mfcc, sq_m, C) != ACOSS_OK || euclid(ssm, d_ssm, sq_s, C + mstride) != ACOSS_OK)
         return ACOSS_E_HIP;
     }
-    hipLaunchKernelGGL(k_ef_csm<1>, dim3((unsigned)(tiles * tiles * P)), dim3(256), 0, s, chn, d_chroma, nullptr, E, oti, ld,
-                       C + 2 * mstride);
+    if (wave_tiles && d_chroma % 24 == 0)
+      hipLaunchKernelGGL(k_ef_csm_w<1>, dim3((unsigned)((tiles * tiles * P + 3) / 4)), dim3(256), 0, s, chn, d_chroma,
+                         nullptr, E, oti, ld, tiles * tiles * P, C + 2 * mstride);
+    else
+      hipLaunchKernelGGL(k_ef_csm<1>, dim3((unsigned)(tiles * tiles * P)), dim3(256), 0, s, chn, d_chroma, nullptr, E,
+                         oti, ld, C + 2 * mstride);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_CSM, s);
     prof_begin(PH_BIN, s);
