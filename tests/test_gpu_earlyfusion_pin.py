@@ -188,3 +188,41 @@ def test_ef_block_features_gpu_vs_restatement():
         npo.ef_block_features(short[0], rng.normal(size=(20, 300)).astype(np.float32), np.arange(1, 300, 90))
     with pytest.raises(ValueError):
         _lib.ef_block_features(short, [rng.normal(size=(300, 20)).astype(np.float32)], [np.arange(1, 300, 90)])
+
+
+_EF_KERNEL_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [sys.argv[1], sys.argv[1] + '/acoss-1_amd']
+from acoss import _lib
+rng = np.random.default_rng(9)
+NT, NB = 7, int(sys.argv[2])
+bank = {'mfccs': torch.as_tensor(rng.standard_normal((NT * NB, 1000), dtype=np.float32)).cuda(),
+        'ssms': torch.as_tensor(np.abs(rng.standard_normal((NT * NB, int(sys.argv[3])), dtype=np.float32))).cuda(),
+        'chromas': torch.as_tensor(np.abs(rng.standard_normal((NT * NB, 480), dtype=np.float32))).cuda(),
+        'chroma_med': torch.as_tensor(np.abs(rng.standard_normal((NT, 12), dtype=np.float32))).cuda(),
+        'off': torch.as_tensor(np.arange(NT, dtype=np.int64) * NB).cuda(),
+        'nb': torch.as_tensor(np.full(NT, NB, np.int32)).cuda(), 'max_blocks': NB}
+pairs = np.array([(i, j) for i in range(NT) for j in range(NT) if i != j], np.int32)
+np.save(sys.argv[4], _lib.earlyfusion(bank, pairs, 0.1, 10).cpu().numpy())
+"""
+
+
+@pytest.mark.parametrize("nb,d_ssm", [(130, 1225), (64, 1000), (71, 1221)])
+def test_earlyfusion_wave_csm_equals_lds_csm(tmp_path, nb, d_ssm):
+    """The wave-tile CSM kernels (k_ef_csm_w: euclid, the padded SSM bank, the cosine chroma CSM
+    with the OTI roll in registers) against the LDS-tiled ones (ACOSS_EF_LDS_CSM=1, read once per
+    process, hence two processes): every EarlyFusion score bit-identical, over all ordered pairs
+    (every OTI roll), ragged tile edges and an SSM width that is not a multiple of 4."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    out = {}
+    for tag, env in (("wave", {}), ("lds", {"ACOSS_EF_LDS_CSM": "1"})):
+        f = str(tmp_path / ("%s.npy" % tag))
+        r = subprocess.run([sys.executable, "-c", _EF_KERNEL_SCRIPT, ROOT, str(nb), str(d_ssm), f],
+                           env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[tag] = np.load(f)
+    assert np.isfinite(out["wave"]).all()
+    np.testing.assert_array_equal(out["wave"], out["lds"])
