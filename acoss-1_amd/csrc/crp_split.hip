@@ -1303,7 +1303,10 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
 // at most short_n codes take LineS<8>; short_n = 0 disables); KQ = 16: as 0 with LineS<16> for
 // the rest (every line <= 1024 codes); KQ = 2: as 0, and rows past 2048 codes take Line2.
 template <int KQ>
-__global__ __launch_bounds__(kThreads, 4) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
+#ifndef ACOSS_SWEEP_WPE
+#define ACOSS_SWEEP_WPE 4
+#endif
+__global__ __launch_bounds__(kThreads, ACOSS_SWEEP_WPE) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
                                                           int64_t kstride, float kappa, float* __restrict__ thr,
                                                           float* __restrict__ Tq, int64_t thr_stride,
                                                           uint32_t* __restrict__ RT, int64_t rt_stride, int ld,
