@@ -348,8 +348,9 @@ __device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int
   const int per = (N + 63) / 64;
   const int c0 = lane * per, c1 = min(N, c0 + per);
   unsigned lo = 0, hi = 0xffffffffu;
-  if (per <= KB) {  // the row's keys in registers: one pass over memory
-    unsigned kr[KB];
+  unsigned kr[KB];
+  const bool inreg = per <= KB;
+  if (inreg) {  // the row's keys in registers: one pass over memory
 #pragma unroll
     for (int q = 0; q < KB; ++q) kr[q] = (q < per && c0 + q < c1) ? fkey(x[c0 + q]) : 0xffffffffu;
     unsigned mn = 0xffffffffu, mx = 0u;  // bound the search by the row's range
@@ -383,6 +384,25 @@ __device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int
   }
   const unsigned kth = lo;
   int less = 0, eq = 0;
+  if (inreg) {  // the keys are still in registers: no second and third read of the row
+#pragma unroll
+    for (int q = 0; q < KB; ++q) {
+      less += kr[q] < kth;
+      eq += kr[q] == kth;
+    }
+    const int take_eq = nn - wave_sum(less);
+    int seen = wave_incl_scan(eq) - eq;
+#pragma unroll
+    for (int q = 0; q < KB; ++q) {
+      bool v = kr[q] < kth;
+      if (kr[q] == kth && q < per && c0 + q < c1) {
+        v = seen < take_eq;
+        ++seen;
+      }
+      if (v) atomicOr(&bits[c0 + q], bit);
+    }
+    return;
+  }
   for (int k = c0; k < c1; ++k) {
     const unsigned kk = fkey(x[k]);
     less += kk < kth;
