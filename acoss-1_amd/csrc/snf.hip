@@ -6,9 +6,9 @@
 // with S_i the kNN-truncated, row-normalised W_i (getS, :121-143): K entries per row.
 // (S A^T)^T = A S^T, so the step is two row-sparse products, both as COALESCED row gathers:
 //   At        = A^T                            (k_snf_avg_t: the average, transposed via LDS)
-//   B         = (S . At)^T                     (k_snf_gather_t: B^T[j, :] = sum_k V[j,k] At[J[j,k], :],
+//   B         = (S . At)^T                     (k_snf_spmm<true>: B^T[j, :] = sum_k V[j,k] At[J[j,k], :],
 //                                               written transposed through an LDS tile)
-//   out[i, :] = sum_k V[i,k] * B[J[i,k], :]    (k_snf_left)
+//   out[i, :] = sum_k V[i,k] * B[J[i,k], :]    (k_snf_spmm<false>)
 // so B[a, j] = sum_k V[j,k] * A[a, J[j,k]], the reference's inner product, term for term.
 // Both products sum over k in ascending column order from 0, one rounded multiply and one
 // rounded add per term (-ffp-contract=off), as scipy's csr_matvecs does on the csr matrix that
@@ -16,8 +16,8 @@
 // is formed in the reference's order (m ascending, then one division). All float64.
 //
 // Traffic per step (n x n float64 each): the transpose reads the L-1 other matrices and writes
-// At; each gather reads K rows per output row (repeated hub rows hit L2/MALL) and writes one
-// matrix. Algorithmic HBM bytes: (L - 1 + 1 + 2 + 2) * 8 * n^2 = (L + 4) * 8 n^2.
+// At; each gather reads K row segments per output row (from the L2 working set of its column
+// chunk, see k_snf_spmm) and writes one matrix. Algorithmic HBM bytes: (L - 1 + 1 + 2 + 2) * 8 * n^2 = (L + 4) * 8 n^2.
 #include "common.hpp"
 
 namespace acoss {
@@ -108,81 +108,90 @@ __global__ __launch_bounds__(256) void k_snf_avg_t(MatPtrs mats, int32_t cnt, in
   }
 }
 
-// B[a, j] = sum_k Vs[j,k] * At[Js[j,k], a] for the stripe's rows a < rows (At is (n, rows), B
-// the (rows, n) stripe of the product). Block = 32 rows j x 64 columns a; each wave takes
-// 8 rows j, lane = column a (each gathered row segment is one 512-byte run), and the 32 x 64
-// result leaves transposed through LDS as 64 runs of 32 doubles. (16-byte loads over 128
-// columns measured slower: 17.2 vs 16.4 ms per step at n = 15,000.)
-constexpr int kGJ = 32;
-__global__ __launch_bounds__(256) void k_snf_gather_t(const double* __restrict__ At, int32_t rows, int32_t n, int32_t K,
-                                                      const int32_t* __restrict__ Js,
-                                                      const double* __restrict__ Vs, double* __restrict__ B) {
-  __shared__ double tile[64][kGJ + 1];
-  const int a0 = blockIdx.x * 64, j0 = blockIdx.y * kGJ;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int a = a0 + lane;
-  const bool aok = a < rows;
-#pragma unroll
-  for (int q = 0; q < kGJ / 4; ++q) {
-    const int jl = w * (kGJ / 4) + q;
-    const int j = j0 + jl;
-    double acc = 0.0;
-    if (j < n) {
-      for (int k = 0; k < K; ++k) {
-        const int32_t row = Js[(int64_t)j * K + k];
-        const double v = Vs[(int64_t)j * K + k];
-        if (aok) acc = acc + v * At[(int64_t)row * rows + a];
-      }
-    }
-    tile[lane][jl] = acc;
+// Both products are row gathers of a dense matrix D by the sparse S (K entries per row):
+//   R[r, c] = sum_k Vs[r,k] * D[Js[r,k], c]   (ascending k, one rounded multiply and add per term)
+// TRANS (gather): D = At (n x rows), r = j in [0, n), written transposed as B[c, j];
+// !TRANS (left):  D = B (n x n), r = i in [row0, row0 + rows), written as out[i - row0, c]
+//                 (+ reg_diag on the diagonal, after the sum, as the reference's separate
+//                 `nextPts[i][pix, pix] += reg_diag`).
+// Tiling for the caches: a block is kSnfRB output rows x kSnfW columns of D, and the blocks are
+// ordered column-chunk-major per XCD (xcd_remap): each XCD walks its own run of chunks, every
+// output row of a chunk before the next, so the K gathered segments of all rows come from that
+// XCD's L2 working set, D[:, chunk] = n x kSnfW doubles (3.8 MB at n = 15,000), instead of
+// the whole of D (1.8 GB, which the first versions gathered from at 4-7 TB/s of HBM/MALL).
+constexpr int kSnfW = 32;   // columns per chunk (lane & 31)
+constexpr int kSnfRB = 32;  // output rows per block (8 row groups of 32 lanes x 4)
+template <bool TRANS>
+__global__ __launch_bounds__(256) void k_snf_spmm(const double* __restrict__ D, int64_t ldd, int32_t dcols,
+                                                  int32_t nout, int32_t row0, int32_t K,
+                                                  const int32_t* __restrict__ Js, const double* __restrict__ Vs,
+                                                  double reg_diag, double* __restrict__ out, int64_t ldo,
+                                                  int32_t rblocks) {
+  __shared__ double tile[TRANS ? kSnfW : 1][kSnfRB + 1];
+  __shared__ int32_t sj[kSnfRB * kSnfMaxK];
+  __shared__ double sv[kSnfRB * kSnfMaxK];
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int chunk = L / rblocks, rb = L - chunk * rblocks;
+  const int cl = threadIdx.x & (kSnfW - 1), rg = threadIdx.x / kSnfW;  // rg: 0..7
+  const int c = chunk * kSnfW + cl;
+  const bool cok = c < dcols;
+  // the block's kNN rows (contiguous in Js/Vs) staged in LDS: the gathers below then issue
+  // without a dependent index load in front of each
+  const int r0 = rb * kSnfRB, nr = min(kSnfRB, nout - r0);
+  for (int t = threadIdx.x; t < nr * K; t += 256) {
+    sj[t] = Js[(int64_t)(row0 + r0) * K + t];
+    sv[t] = Vs[(int64_t)(row0 + r0) * K + t];
   }
   __syncthreads();
+  const double* Dc = D + (cok ? c : 0);
 #pragma unroll
-  for (int r = 0; r < (64 * kGJ) / 256; ++r) {
-    const int idx = threadIdx.x + 256 * r;
-    const int al = idx / kGJ, jl = idx % kGJ;
-    const int aa = a0 + al, j = j0 + jl;
-    if (aa < rows && j < n) B[(int64_t)aa * n + j] = tile[al][jl];
+  for (int q = 0; q < kSnfRB / 8; ++q) {
+    const int rl = rg + 8 * q;
+    const int r = r0 + rl;  // output row (0-based within the output)
+    double acc = 0.0;
+    if (rl < nr) {
+      const int i = row0 + r;  // kNN row
+      const int32_t* jr = sj + rl * K;
+      const double* vr = sv + rl * K;
+      int k = 0;
+      for (; k + 4 <= K; k += 4) {  // four gathers in flight, summed in k order
+        const double x0 = Dc[(int64_t)jr[k] * ldd], x1 = Dc[(int64_t)jr[k + 1] * ldd];
+        const double x2 = Dc[(int64_t)jr[k + 2] * ldd], x3 = Dc[(int64_t)jr[k + 3] * ldd];
+        acc = acc + vr[k] * x0;
+        acc = acc + vr[k + 1] * x1;
+        acc = acc + vr[k + 2] * x2;
+        acc = acc + vr[k + 3] * x3;
+      }
+      for (; k < K; ++k) acc = acc + vr[k] * Dc[(int64_t)jr[k] * ldd];
+      if (!TRANS && cok) {
+        if (c == i && reg_diag > 0.0) acc = acc + reg_diag;
+        out[(int64_t)r * ldo + c] = acc;
+      }
+    }
+    if (TRANS) tile[cl][rl] = acc;
+  }
+  if constexpr (TRANS) {
+    __syncthreads();
+    // B[c, r]: kSnfW runs of kSnfRB consecutive doubles
+#pragma unroll
+    for (int t = 0; t < (kSnfW * kSnfRB) / 256; ++t) {
+      const int idx = threadIdx.x + 256 * t;
+      const int cc = idx / kSnfRB, rr = idx % kSnfRB;
+      const int oc = chunk * kSnfW + cc, orow = rb * kSnfRB + rr;
+      if (oc < dcols && orow < nout) out[(int64_t)oc * ldo + orow] = tile[cc][rr];
+    }
   }
 }
 
-// out[i, j] = sum_k Vs[i,k] * B[Js[i,k], j] (+ reg_diag on the diagonal, added after the sum
-// as the reference's separate `nextPts[i][pix, pix] += reg_diag`) for the rows i of the stripe
-// [row0, row0 + gridDim.y); out is that (rows, n) stripe, B the whole (n, n) product.
-// Block = row i x 1024 columns, 4 consecutive columns per thread as two 16-byte loads per row.
-__global__ __launch_bounds__(256) void k_snf_left(const double* __restrict__ B, int32_t n, int32_t row0, int32_t K,
-                                                  const int32_t* __restrict__ Js, const double* __restrict__ Vs,
-                                                  double reg_diag, double* __restrict__ out) {
-  const int i = row0 + blockIdx.y;
-  const int j0 = (blockIdx.x * 256 + threadIdx.x) * 4;
-  if (j0 >= n) return;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  const bool full = (j0 + 4 <= n) && ((n & 1) == 0);
-  for (int k = 0; k < K; ++k) {
-    const int32_t row = Js[(int64_t)i * K + k];
-    const double v = Vs[(int64_t)i * K + k];
-    const double* src = B + (int64_t)row * n + j0;
-    if (full) {
-      const double2 x0 = *reinterpret_cast<const double2*>(src);
-      const double2 x1 = *reinterpret_cast<const double2*>(src + 2);
-      acc[0] = acc[0] + v * x0.x;
-      acc[1] = acc[1] + v * x0.y;
-      acc[2] = acc[2] + v * x1.x;
-      acc[3] = acc[3] + v * x1.y;
-    } else {
-      for (int t = 0; t < 4; ++t)
-        if (j0 + t < n) acc[t] = acc[t] + v * src[t];
-    }
-  }
-  double* dst = out + (int64_t)blockIdx.y * n + j0;
-  for (int t = 0; t < 4; ++t) {
-    const int j = j0 + t;
-    if (j < n) {
-      double x = acc[t];
-      if (j == i && reg_diag > 0.0) x = x + reg_diag;
-      dst[t] = x;
-    }
-  }
+// Launch of k_snf_spmm over nout output rows and dcols columns of D.
+template <bool TRANS>
+int snf_spmm(const double* D, int64_t ldd, int32_t dcols, int32_t nout, int32_t row0, int32_t K, const int32_t* Js,
+             const double* Vs, double reg_diag, double* out, int64_t ldo, hipStream_t s) {
+  const int32_t rblocks = (nout + kSnfRB - 1) / kSnfRB, nchunks = (dcols + kSnfW - 1) / kSnfW;
+  hipLaunchKernelGGL(k_snf_spmm<TRANS>, dim3((unsigned)rblocks * (unsigned)nchunks), dim3(256), 0, s, D, ldd, dcols,
+                     nout, row0, K, Js, Vs, reg_diag, out, ldo, rblocks);
+  ACOSS_LAUNCH_CHECK();
+  return ACOSS_OK;
 }
 
 }  // namespace
@@ -248,9 +257,8 @@ int snf_diffuse(const double* const* mats, int32_t n_mats, int32_t skip, int32_t
       cnt = 0;
     }
   }
-  hipLaunchKernelGGL(k_snf_gather_t, dim3(nr, (n + kGJ - 1) / kGJ), dim3(256), 0, s, At, rows, n, K, Js, Vs, B);
-  ACOSS_LAUNCH_CHECK();
-  return ACOSS_OK;
+  // B[a, j] = sum_k Vs[j,k] * At[Js[j,k], a]: rows j of S over the stripe's columns a of At
+  return snf_spmm<true>(At, rows, rows, n, 0, K, Js, Vs, 0.0, B, n, s);
 }
 
 bool overlaps(const double* a, size_t na, const double* b, size_t nb) {
@@ -285,9 +293,7 @@ extern "C" int acoss_snf_step(const double* const* mats, int32_t n_mats, int32_t
   double* At = reinterpret_cast<double*>(ws + nn * 8);
   rc = snf_diffuse(mats, n_mats, skip, n, n, Js, Vs, K, At, Bm, s);
   if (rc != ACOSS_OK) return rc;
-  hipLaunchKernelGGL(k_snf_left, dim3((n + 1023) / 1024, n), dim3(256), 0, s, Bm, n, 0, K, Js, Vs, reg_diag, out);
-  ACOSS_LAUNCH_CHECK();
-  return ACOSS_OK;
+  return snf_spmm<false>(Bm, n, n, n, 0, K, Js, Vs, reg_diag, out, n, s);
 }
 
 extern "C" int acoss_snf_diffuse_rows(const double* const* mats, int32_t n_mats, int32_t skip, int32_t n,
@@ -335,8 +341,5 @@ extern "C" int acoss_snf_left_rows(const double* B, int32_t n, int32_t row0, int
   double* Vs = nullptr;
   int rc = snf_sorted_knn(J, V, n, K, validate, 0, s, &ws, &Js, &Vs);
   if (rc != ACOSS_OK) return rc;
-  hipLaunchKernelGGL(k_snf_left, dim3((n + 1023) / 1024, rows), dim3(256), 0, s, B, n, row0, K, Js, Vs, reg_diag,
-                     out);
-  ACOSS_LAUNCH_CHECK();
-  return ACOSS_OK;
+  return snf_spmm<false>(B, n, n, rows, row0, K, Js, Vs, reg_diag, out, n, s);
 }

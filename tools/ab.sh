@@ -35,7 +35,9 @@ for v in "$@"; do
   fi
   for e in "${ENVS[@]}"; do
     echo "variant=$v env=[$e]"
-    env $e ACOSS_HIP_LIB=$PWD/$L timeout -k 10 180 $KB --noprof 2>&1 | grep -E "rep $last|checksum" || exit 1
-    env $e ACOSS_SPLIT_STREAMS=1 ACOSS_HIP_LIB=$PWD/$L timeout -k 10 180 $KB 2>&1 | grep -E "rep $last" || exit 1
+    env $e ACOSS_HIP_LIB=$PWD/$L timeout -k 10 180 $KB --noprof > gpurun_out/ab_run.log 2>&1 || { tail -5 gpurun_out/ab_run.log; exit 1; }
+    grep -E "rep $last|checksum" gpurun_out/ab_run.log
+    env $e ACOSS_SPLIT_STREAMS=1 ACOSS_HIP_LIB=$PWD/$L timeout -k 10 180 $KB > gpurun_out/ab_run.log 2>&1 || { tail -5 gpurun_out/ab_run.log; exit 1; }
+    grep -E "rep $last" gpurun_out/ab_run.log
   done
 done
