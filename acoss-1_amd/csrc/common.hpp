@@ -135,10 +135,18 @@ __host__ __device__ inline float next_down(float x) {
   unsigned u = __builtin_bit_cast(unsigned, x);
   return u == 0u ? x : __builtin_bit_cast(float, u - 1u);
 }
+// Closed form (no search): with up = next_up(thr) and m = (thr + up) / 2 (exact in double),
+// sqrt_rn(T) <= thr  <=>  T < m^2, or T == m^2 and the tie rounds to thr (thr's last bit even).
+// m has at most 26 significant bits, so m^2 is exact in double; T is m^2 rounded down to float,
+// stepped down once more on an exact tie that rounds up. (The two 16-step searches this replaces
+// unrolled into ~100 instructions per line of the selects; tests/test_sq_threshold.py checks the
+// closed form against the search.)
 __device__ inline float sq_threshold(float thr) {
-  float t = thr * thr;
-  for (int it = 0; it < 16 && t > 0.0f && sqrt_rn(t) > thr; ++it) t = next_down(t);
-  for (int it = 0; it < 16 && sqrt_rn(next_up(t)) <= thr; ++it) t = next_up(t);
+  const double m = ((double)thr + (double)next_up(thr)) * 0.5;
+  const double m2 = m * m;
+  float t = (float)m2;             // round to nearest
+  if ((double)t > m2) t = next_down(t);  // -> round down
+  if ((double)t == m2 && (__builtin_bit_cast(unsigned, thr) & 1u)) t = next_down(t);
   return t;
 }
 

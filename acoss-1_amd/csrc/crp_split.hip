@@ -351,6 +351,20 @@ __device__ __forceinline__ unsigned pk_subsat_u16(unsigned a, unsigned b) {
   return __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
 }
 
+// Smallest prefix > x (x < kNone) among a lane's packed words, or 0xffffffff: per field
+// (k - x - 1) mod 2^16 (one wrapping packed add) puts every real k > x at k - x - 1 <= 0x7f80 - x - 1,
+// kNone at 0x7fff - x - 1 and every k <= x at >= 0x10000 - x - 1, so a packed minimum and one
+// compare find it (2 VALU per word; the per-element compare/select form took ~7 per element).
+template <int NW>
+__device__ __forceinline__ unsigned swar_min_greater(const unsigned (&pv)[NW], unsigned x) {
+  const unsigned X = ((0x10000u - x - 1u) & 0xffffu) * 0x10001u;
+  unsigned a = 0xffffffffu;
+#pragma unroll
+  for (int h = 0; h < NW; ++h) a = pk_min_u16(a, pk_add_u16(pv[h], X));
+  const unsigned d = min(a & 0xffffu, a >> 16);
+  return d < kNone - x - 1u ? d + x + 1u : 0xffffffffu;
+}
+
 // Bits h, h + 8, h + 16, h + 24 of the result take the flags (bits 7, 15, 23, 31) of word h.
 __device__ __forceinline__ uint32_t gather_flags8(uint32_t acc, uint32_t s, int h) {
   return ((s >> (7 - h)) & (0x01010101u << h)) | acc;
@@ -545,15 +559,7 @@ struct Line {
     const unsigned m = wave_max_u32(b);
     *mx = m ? m - 1 : 0u;
   }
-  __device__ __forceinline__ unsigned min_greater_lane(unsigned x) const {
-    unsigned a = 0xffffffffu;
-#pragma unroll
-    for (int q = 0; q < KPL; ++q) {
-      const unsigned k = pfx(q);
-      a = (k > x && k != kNone) ? min(a, k) : a;
-    }
-    return a;
-  }
+  __device__ __forceinline__ unsigned min_greater_lane(unsigned x) const { return swar_min_greater(pv, x); }
   __device__ __forceinline__ unsigned min_greater(unsigned x) const { return wave_min_u32(min_greater_lane(x)); }
   static constexpr int kHalves = 1;
 };
@@ -698,15 +704,7 @@ struct LineS {
     const unsigned m = wave_max_u32(b);
     *mx = m ? m - 1 : 0u;
   }
-  __device__ __forceinline__ unsigned min_greater(unsigned x) const {
-    unsigned a = 0xffffffffu;
-#pragma unroll
-    for (int q = 0; q < KQ; ++q) {
-      const unsigned k = pfx(q);
-      a = (k > x && k != kNone) ? min(a, k) : a;
-    }
-    return wave_min_u32(a);
-  }
+  __device__ __forceinline__ unsigned min_greater(unsigned x) const { return wave_min_u32(swar_min_greater(pv, x)); }
 };
 
 // Lane t's 32-bit line word t (elements 32 t .. 32 t + 31) from a short line's per-lane mask:

@@ -119,22 +119,26 @@ __global__ __launch_bounds__(256) void k_snf_avg_t(MatPtrs mats, int32_t cnt, in
 // output row of a chunk before the next, so the K gathered segments of all rows come from that
 // XCD's L2 working set, D[:, chunk] = n x kSnfW doubles (3.8 MB at n = 15,000), instead of
 // the whole of D (1.8 GB, which the first versions gathered from at 4-7 TB/s of HBM/MALL).
-constexpr int kSnfW = 32;   // columns per chunk (lane & 31)
-constexpr int kSnfRB = 32;  // output rows per block (8 row groups of 32 lanes x 4)
-template <bool TRANS>
+constexpr int kSnfW = 32;   // columns per chunk
+constexpr int kSnfRB = 32;  // output rows per block
+// VW consecutive columns per lane (VW = 2: 16-byte gathers, 16 lanes per row segment, when the
+// row pitch and the column count are even); 256 / (kSnfW / VW) row groups per pass.
+template <bool TRANS, int VW>
 __global__ __launch_bounds__(256) void k_snf_spmm(const double* __restrict__ D, int64_t ldd, int32_t dcols,
                                                   int32_t nout, int32_t row0, int32_t K,
                                                   const int32_t* __restrict__ Js, const double* __restrict__ Vs,
                                                   double reg_diag, double* __restrict__ out, int64_t ldo,
                                                   int32_t rblocks) {
+  constexpr int LPR = kSnfW / VW, RG = 256 / LPR;  // lanes per row segment, row groups
+  typedef double dvec __attribute__((ext_vector_type(VW)));
   __shared__ double tile[TRANS ? kSnfW : 1][kSnfRB + 1];
   __shared__ int32_t sj[kSnfRB * kSnfMaxK];
   __shared__ double sv[kSnfRB * kSnfMaxK];
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int chunk = L / rblocks, rb = L - chunk * rblocks;
-  const int cl = threadIdx.x & (kSnfW - 1), rg = threadIdx.x / kSnfW;  // rg: 0..7
+  const int cl = (threadIdx.x % LPR) * VW, rg = threadIdx.x / LPR;
   const int c = chunk * kSnfW + cl;
-  const bool cok = c < dcols;
+  const bool cok = c < dcols;  // VW = 2: dcols is even, so c + 1 < dcols too
   // the block's kNN rows (contiguous in Js/Vs) staged in LDS: the gathers below then issue
   // without a dependent index load in front of each
   const int r0 = rb * kSnfRB, nr = min(kSnfRB, nout - r0);
@@ -143,32 +147,38 @@ __global__ __launch_bounds__(256) void k_snf_spmm(const double* __restrict__ D, 
     sv[t] = Vs[(int64_t)(row0 + r0) * K + t];
   }
   __syncthreads();
-  const double* Dc = D + (cok ? c : 0);
+  const dvec* Dc = reinterpret_cast<const dvec*>(D + (cok ? c : 0));
+  const int64_t ldv = ldd / VW;
 #pragma unroll
-  for (int q = 0; q < kSnfRB / 8; ++q) {
-    const int rl = rg + 8 * q;
+  for (int q = 0; q < kSnfRB / RG; ++q) {
+    const int rl = rg + RG * q;
     const int r = r0 + rl;  // output row (0-based within the output)
-    double acc = 0.0;
+    dvec acc = 0.0;
     if (rl < nr) {
       const int i = row0 + r;  // kNN row
       const int32_t* jr = sj + rl * K;
       const double* vr = sv + rl * K;
       int k = 0;
       for (; k + 4 <= K; k += 4) {  // four gathers in flight, summed in k order
-        const double x0 = Dc[(int64_t)jr[k] * ldd], x1 = Dc[(int64_t)jr[k + 1] * ldd];
-        const double x2 = Dc[(int64_t)jr[k + 2] * ldd], x3 = Dc[(int64_t)jr[k + 3] * ldd];
+        const dvec x0 = Dc[jr[k] * ldv], x1 = Dc[jr[k + 1] * ldv];
+        const dvec x2 = Dc[jr[k + 2] * ldv], x3 = Dc[jr[k + 3] * ldv];
         acc = acc + vr[k] * x0;
         acc = acc + vr[k + 1] * x1;
         acc = acc + vr[k + 2] * x2;
         acc = acc + vr[k + 3] * x3;
       }
-      for (; k < K; ++k) acc = acc + vr[k] * Dc[(int64_t)jr[k] * ldd];
+      for (; k < K; ++k) acc = acc + vr[k] * Dc[jr[k] * ldv];
       if (!TRANS && cok) {
-        if (c == i && reg_diag > 0.0) acc = acc + reg_diag;
-        out[(int64_t)r * ldo + c] = acc;
+#pragma unroll
+        for (int v = 0; v < VW; ++v)
+          if (c + v == i && reg_diag > 0.0) acc[v] = acc[v] + reg_diag;
+        *reinterpret_cast<dvec*>(out + (int64_t)r * ldo + c) = acc;
       }
     }
-    if (TRANS) tile[cl][rl] = acc;
+    if (TRANS) {
+#pragma unroll
+      for (int v = 0; v < VW; ++v) tile[cl + v][rl] = acc[v];
+    }
   }
   if constexpr (TRANS) {
     __syncthreads();
@@ -188,8 +198,12 @@ template <bool TRANS>
 int snf_spmm(const double* D, int64_t ldd, int32_t dcols, int32_t nout, int32_t row0, int32_t K, const int32_t* Js,
              const double* Vs, double reg_diag, double* out, int64_t ldo, hipStream_t s) {
   const int32_t rblocks = (nout + kSnfRB - 1) / kSnfRB, nchunks = (dcols + kSnfW - 1) / kSnfW;
-  hipLaunchKernelGGL(k_snf_spmm<TRANS>, dim3((unsigned)rblocks * (unsigned)nchunks), dim3(256), 0, s, D, ldd, dcols,
-                     nout, row0, K, Js, Vs, reg_diag, out, ldo, rblocks);
+  static const char* vwenv = getenv("ACOSS_SNF_VW");
+  const bool even = ldd % 2 == 0 && dcols % 2 == 0 && (TRANS || ldo % 2 == 0);
+  const bool v2 = even && !(vwenv && vwenv[0] == '1');
+  auto kern = v2 ? k_snf_spmm<TRANS, 2> : k_snf_spmm<TRANS, 1>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)rblocks * (unsigned)nchunks), dim3(256), 0, s, D, ldd, dcols, nout, row0, K,
+                     Js, Vs, reg_diag, out, ldo, rblocks);
   ACOSS_LAUNCH_CHECK();
   return ACOSS_OK;
 }
