@@ -23,6 +23,7 @@
 //    pass down one lane per step with __shfl_up; bands chain through a small HBM buffer.
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "crp_internal.hpp"
 
@@ -1203,7 +1204,15 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
     const int v = e ? atoi(e) : 2;
     return v < 1 ? 1 : (v > 3 ? 3 : v);
   }();
-  char* ws = static_cast<char*>(workspace(1, slot * nb_alloc + (split ? nbuf * sub_pair * sub : 0) + 8192));
+  // fused launches (k_sweep_cols9: a sub-batch's sweep and the previous one's column select in one
+  // grid, on the caller's stream) replace the side streams unless ACOSS_SPLIT_FUSED=0; they need
+  // the two plane buffers of the two-stream mode
+  const char* fused_env = getenv("ACOSS_SPLIT_FUSED");
+  const bool fused = split && nbuf >= 2 && !(fused_env && fused_env[0] == '0');
+  // fused launches alternate between two streams, launch k pairing sub-batch k's sweep with
+  // sub-batch k-2's select (same stream): four plane buffers keep every writer and reader apart
+  const int nkb = fused ? 4 : nbuf;
+  char* ws = static_cast<char*>(workspace(1, slot * nb_alloc + (split ? nkb * sub_pair * sub : 0) + 8192));
   if (!ws) return ACOSS_E_HIP;
   size_t o = 0;
   auto carve = [&](size_t bytes) {
@@ -1220,9 +1229,9 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   uint32_t* w_mask = reinterpret_cast<uint32_t*>(carve(4 * mask_stride * nb_alloc));
   float4* w_bnd = reinterpret_cast<float4*>(carve(16 * bnd_stride * nb_alloc));
   float* w_yrot = reinterpret_cast<float*>(carve(4 * yrot_stride * nb_alloc));
-  void* w_kpl[3] = {nullptr, nullptr, nullptr};
-  uint32_t* w_rt[3] = {nullptr, nullptr, nullptr};
-  for (int b = 0; split && b < nbuf; ++b) {
+  void* w_kpl[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint32_t* w_rt[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int b = 0; split && b < nkb; ++b) {
     w_kpl[b] = static_cast<void*>(carve(4 * (size_t)kstride * sub));
     w_rt[b] = reinterpret_cast<uint32_t*>(carve(4 * (size_t)mask_stride * sub));
   }
@@ -1256,7 +1265,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
     }
   }
   hipStream_t ss[3] = {s, s, s};
-  for (int b = 1; split && b < nbuf; ++b) {
+  for (int b = 1; split && b < (fused ? 2 : nbuf); ++b) {
     ss[b] = side_stream(b - 1);
     if (!ss[b]) {
       set_error("could not create the side stream");
@@ -1276,7 +1285,42 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
                        yrot_stride);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_OTI, s);
-    if (split) {
+    if (split && fused) {
+      // launch k (stream k % 2): sub-batch k's sweep (plane buffer k % 4) with sub-batch k - 2's
+      // column select (buffer (k - 2) % 4, swept by launch k - 2 on the same stream); two more
+      // launches finish the last two selects
+      const int nsb = (int)((nb + sub - 1) / sub);
+      hipEvent_t e0 = sync_event(0);
+      ACOSS_HIP_CHECK(hipEventRecord(e0, s));
+      ACOSS_HIP_CHECK(hipStreamWaitEvent(ss[1], e0, 0));
+      std::vector<SplitSide> sides((size_t)nsb);
+      for (int k = 0; k < nsb + 2; ++k) {
+        SplitSide cur{}, old{};
+        cur.nb = old.nb = 0;
+        if (k < nsb) {
+          const int s0 = (int)(k * sub);
+          const int ns = (nb - s0) < sub ? (nb - s0) : (int)sub;
+          const int b = k & 3;
+          cur = SplitSide{CrpBatch{feats, X2, track_off, track_len, NX, ldn, pb + 2 * s0, w_oti + s0, w_dims + s0, m,
+                                   tau, w_yrot + (size_t)s0 * yrot_stride, yrot_stride},
+                          ns, w_kpl[b], rings[b & 1], w_rt[b],
+                          w_thr_r + (size_t)s0 * thr_stride, w_T_r + (size_t)s0 * thr_stride,
+                          w_thr_c + (size_t)s0 * thr_stride, w_T_c + (size_t)s0 * thr_stride,
+                          w_mask + (size_t)s0 * mask_stride};
+          sides[(size_t)k] = cur;
+        }
+        if (k >= 2) old = sides[(size_t)(k - 2)];
+        if (cur.nb == 0 && old.nb == 0) continue;
+        if (cur.nb == 0) cur.B = old.B;
+        if (old.nb == 0) old.B = cur.B;
+        if ((rc = launch_crp_split_fused(cur, old, L, params->kappa, ldk, kstride, thr_stride, mask_stride, ld,
+                                         ss[k & 1])))
+          return rc;
+      }
+      hipEvent_t e1 = sync_event(1);  // the DP (caller's stream) needs both streams' launches
+      ACOSS_HIP_CHECK(hipEventRecord(e1, ss[1]));
+      ACOSS_HIP_CHECK(hipStreamWaitEvent(s, e1, 0));
+    } else if (split) {
       const int nsb = (int)((nb + sub - 1) / sub);     // sub-batches of this batch
       const int nst = nbuf < nsb ? nbuf : nsb;         // streams they rotate over
       if (nst > 1) {  // the side streams start after this batch's OTI / roll on the caller's stream

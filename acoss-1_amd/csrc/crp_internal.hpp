@@ -50,6 +50,21 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
                      uint32_t* RT, float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride,
                      uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s);
 
+// One side of a fused split launch (launch_crp_split_fused): a sub-batch of nb pairs (nb = 0:
+// none), its key planes and row-threshold words, and the outputs of its kernel (the row
+// thresholds for the sweep side; the column thresholds and CRP words for the select side).
+struct SplitSide {
+  CrpBatch B;
+  int nb;
+  void* kpl;
+  HrRing ring;
+  uint32_t* RT;
+  float *thr_r, *T_r, *thr_c, *T_c;
+  uint32_t* maskT;
+};
+int launch_crp_split_fused(const SplitSide& S, const SplitSide& C, int L, float kappa, int ldk, int64_t kstride,
+                           int64_t thr_stride, int64_t mask_stride, int ld, hipStream_t s);
+
 int launch_select16(bool trans, const CrpBatch& B, int nb, int L, float kappa, float* thr, float* T,
                     int64_t thr_stride, hipStream_t s);
 

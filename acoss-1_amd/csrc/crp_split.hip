@@ -1300,23 +1300,59 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
 // KQ = 8: every line of the launch is short; KQ = 0: each pair picks its row line type (rows of
 // at most short_n codes take LineS<8>; short_n = 0 disables); KQ = 16: as 0 with LineS<16> for
 // the rest (every line <= 1024 codes); KQ = 2: as 0, and rows past 2048 codes take Line2.
-template <int KQ>
 #ifndef ACOSS_SWEEP_WPE
 #define ACOSS_SWEEP_WPE 4
 #endif
-__global__ __launch_bounds__(kThreads, ACOSS_SWEEP_WPE) void k_sweep_rows9(CrpBatch B, KeyPlanes K, int ldr, int ldc,
-                                                          int64_t kstride, float kappa, float* __restrict__ thr,
-                                                          float* __restrict__ Tq, int64_t thr_stride,
-                                                          uint32_t* __restrict__ RT, int64_t rt_stride, int ld,
-                                                          int short_n) {
+// Arguments of one sweep + row-select launch (k_sweep_rows9) and of one column-select launch
+// (k_sel_cols9); the fused launch (k_sweep_cols9) takes one of each.
+struct SweepArgs {
+  CrpBatch B;
+  KeyPlanes K;
+  int ldr, ldc;
+  int64_t kstride;
+  float kappa;
+  float* thr;
+  float* Tq;
+  int64_t thr_stride;
+  uint32_t* RT;
+  int64_t rt_stride;
+  int ld, short_n;
+};
+struct ColsArgs {
+  CrpBatch B;
+  KeyPlanes K;
+  int ldc;
+  int64_t kstride;
+  float kappa;
+  const uint32_t* RT;
+  float* thr;
+  float* Tq;
+  int64_t thr_stride;
+  uint32_t* maskT;
+  int64_t mask_stride;
+  int ld, short_n;
+};
+template <int KQ>
+constexpr int kSweepLds = KQ == 2 ? kRowsLds2 : kRowsLds;
+
+// One (32-row strip, pair) block of the sweep and its fused row select; smem: kSweepLds<KQ> bytes
+// plus one int (the ring slot).
+template <int KQ>
+__device__ __forceinline__ void sweep_rows_block(const SweepArgs& A, int strip, int p, char* smem, int* s_slot_p) {
   constexpr int RB = KQ == 2 ? 128 : 64;  // row-bit words per row
-  __shared__ __attribute__((aligned(16))) char smem[KQ == 2 ? kRowsLds2 : kRowsLds];
-  const int p = blockIdx.y;
+  const CrpBatch& B = A.B;
+  const KeyPlanes& K = A.K;
+  const int ldr = A.ldr, ldc = A.ldc, ld = A.ld, short_n = A.short_n;
+  const int64_t kstride = A.kstride, thr_stride = A.thr_stride, rt_stride = A.rt_stride;
+  const float kappa = A.kappa;
+  float* thr = A.thr;
+  float* Tq = A.Tq;
+  uint32_t* RT = A.RT;
   const PairView V = pair_view(B, p);
-  const int strip = blockIdx.x, i0 = strip * kSR;
+  const int i0 = strip * kSR;
   if (i0 >= V.Mp || V.Np <= 0) return;
   // the strip's row-major plane: per pair, or a slot of this XCD's ring (HrRing)
-  __shared__ int s_slot;
+  int& s_slot = *s_slot_p;
   uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
   if (K.ring.slots) {
     if (threadIdx.x == 0) {
@@ -1364,6 +1400,13 @@ __global__ __launch_bounds__(kThreads, ACOSS_SWEEP_WPE) void k_sweep_rows9(CrpBa
   ACOSS_STAMP(r1);
   ACOSS_STAMP_ADD(4, r0, r1);  // row select
   if (threadIdx.x == 0) ACOSS_STAMP_ADD(5, 0ull, 1ull);
+}
+
+template <int KQ>
+__global__ __launch_bounds__(kThreads, ACOSS_SWEEP_WPE) void k_sweep_rows9(SweepArgs A) {
+  __shared__ __attribute__((aligned(16))) char smem[kSweepLds<KQ>];
+  __shared__ int s_slot;
+  sweep_rows_block<KQ>(A, blockIdx.x, blockIdx.y, smem, &s_slot);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1475,18 +1518,24 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
 // KQ = 8: every line of the launch is short (runs of kCPW<8> columns); KQ = 0: runs of kCPW<0>,
 // each pair picking its column line type (columns of at most short_n codes take LineS<8>);
 // KQ = 16: as 0 with LineS<16> for the rest; KQ = 2: as 0, and columns past 2048 codes take Line2.
+// One column-select block: linear index lin of nblk = ncb * nb blocks (ncb column blocks per
+// pair), lin % 8 being the XCD the block runs on.
 template <int KQ>
-__global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, KeyPlanes K, int ldc, int64_t kstride, float kappa,
-                                                   const uint32_t* __restrict__ RT, float* __restrict__ thr,
-                                                   float* __restrict__ Tq, int64_t thr_stride,
-                                                   uint32_t* __restrict__ maskT, int64_t mask_stride, int ld,
-                                                   int short_n) {
-  __shared__ WaveLds wl[4];
+__device__ __forceinline__ void cols_block(const ColsArgs& A, int lin, int ncb, int nblk, WaveLds* wl) {
+  const CrpBatch& B = A.B;
+  const KeyPlanes& K = A.K;
+  const int ldc = A.ldc, ld = A.ld, short_n = A.short_n;
+  const int64_t kstride = A.kstride, thr_stride = A.thr_stride, mask_stride = A.mask_stride;
+  const float kappa = A.kappa;
+  const uint32_t* RT = A.RT;
+  float* thr = A.thr;
+  float* Tq = A.Tq;
+  uint32_t* maskT = A.maskT;
   // neighbouring columns share the lines of RT and the recomputed cells' frames: keep them on one XCD
-  const int lb = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-  const int p = lb / gridDim.x;
+  const int lb = xcd_remap(lin, nblk);
+  const int p = lb / ncb;
   const PairView V = pair_view(B, p);
-  const int j0 = (lb - p * gridDim.x) * kColsPerBlock<KQ> + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCPW<KQ>;
+  const int j0 = (lb - p * ncb) * kColsPerBlock<KQ> + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCPW<KQ>;
   const int jend = min(j0 + kCPW<KQ>, V.Np);
   WaveLds& W = wl[threadIdx.x >> 6];
   if (KQ == 8 || V.Mp <= short_n)
@@ -1499,38 +1548,120 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(CrpBatch B, K
     cols_body<0>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
 }
 
+template <int KQ>
+__global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(ColsArgs A) {
+  __shared__ WaveLds wl[4];
+  cols_block<KQ>(A, blockIdx.y * gridDim.x + blockIdx.x, gridDim.x, gridDim.x * gridDim.y, wl);
+}
+
+// Fused launch: the sweep + row select of one sub-batch (nS blocks) and the column select of the
+// previous one (nC blocks) in ONE grid, so every CU holds a mix of the store-heavy walks and the
+// VALU-heavy selects instead of whatever one kernel leaves free for the other. Blocks come in
+// groups of 8 of one kind (8 consecutive blocks land on the 8 XCDs, so a select block's linear
+// index stays congruent to its XCD for xcd_remap), the kinds interleaved in proportion to their
+// group counts (Bresenham), so both progress together through the launch.
+template <int KQ>
+__global__ __launch_bounds__(kThreads, ACOSS_SWEEP_WPE) void k_sweep_cols9(SweepArgs S, int nstrips, int nS,
+                                                                           ColsArgs C, int ncb, int nC) {
+  __shared__ __attribute__((aligned(16))) char smem[kSweepLds<KQ> > (int)(4 * sizeof(WaveLds)) ? kSweepLds<KQ>
+                                                                                               : (int)(4 * sizeof(WaveLds))];
+  __shared__ int s_slot;
+  const int gS = (nS + 7) >> 3, gC = (nC + 7) >> 3, gT = gS + gC;
+  const int b = blockIdx.x, g = b >> 3, x = b & 7;
+  const int s0 = (int)(((int64_t)g * gS) / gT), s1 = (int)(((int64_t)(g + 1) * gS) / gT);
+  if (s1 > s0) {  // a sweep group
+    const int v = 8 * s0 + x;
+    if (v < nS) sweep_rows_block<KQ>(S, v % nstrips, v / nstrips, smem, &s_slot);
+  } else {
+    const int c = 8 * (g - s0) + x;
+    if (c < nC) cols_block<KQ>(C, c, ncb, nC, reinterpret_cast<WaveLds*>(smem));
+  }
+}
+
 }  // namespace
 
 // Two-kernel CRP (m = 9, tau = 1, lines up to 4096 keys). Returns 1 if not applicable.
 // kplanes: nb * kstride uint16 row-major prefixes, then nb * kstride uint16 strip-major ones;
 // RT: nb * mask_stride
 // words (same layout as maskT).
+// Line type of the selects of a launch (by the batch's longest stacked line L): 8 / 16 short lines,
+// 2 some line past 2048 codes, 0 the long-line layout.
+static int split_kq(int L, int* short_n) {
+  static const bool no_short = getenv("ACOSS_NO_SHORT") != nullptr;
+  *short_n = no_short ? 0 : 512;
+  return L > 2048 ? 2 : (no_short ? 0 : (L <= 512 ? 8 : (L <= 1024 ? 16 : 0)));
+}
+
+static SweepArgs sweep_args(const CrpBatch& B, void* kplanes, const HrRing& ring, int ldk, int64_t kstride, int nb,
+                            float kappa, float* thr_r, float* T_r, int64_t thr_stride, uint32_t* RT,
+                            int64_t mask_stride, int ld, int short_n) {
+  const size_t plane = (size_t)nb * kstride;
+  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane, ring};
+  return SweepArgs{B, K, ldk, ldk, kstride, kappa, thr_r, T_r, thr_stride, RT, mask_stride, ld, short_n};
+}
+
+static ColsArgs cols_args(const CrpBatch& B, void* kplanes, int ldk, int64_t kstride, int nb, float kappa,
+                          const uint32_t* RT, float* thr_c, float* T_c, int64_t thr_stride, uint32_t* maskT,
+                          int64_t mask_stride, int ld, int short_n) {
+  const size_t plane = (size_t)nb * kstride;
+  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane, HrRing{}};
+  return ColsArgs{B, K, ldk, kstride, kappa, RT, thr_c, T_c, thr_stride, maskT, mask_stride, ld, short_n};
+}
+
+// Two-kernel CRP (m = 9, tau = 1, lines up to 4096 keys). Returns 1 if not applicable.
+// kplanes: nb * kstride uint16 row-major prefixes, then nb * kstride uint16 strip-major ones;
+// RT: nb * mask_stride words (same layout as maskT).
 int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, const HrRing& ring, int ldk,
                      int64_t kstride,
                      uint32_t* RT, float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride,
                      uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s) {
   if (B.m != kMS || B.tau != 1 || L > 4096) return 1;
-  const size_t plane = (size_t)nb * kstride;
-  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane, ring};
   const int nstrips = (L + kSR - 1) / kSR;
-  // launches whose lines all fit 512 / 1024 codes take LineS<8> / LineS<16> throughout; in
-  // mixed launches each pair picks per side (lines of <= short_n codes LineS<8>, past 2048
-  // Line2, the rest Line<32>)
-  static const bool no_short = getenv("ACOSS_NO_SHORT") != nullptr;
-  const int short_n = no_short ? 0 : 512;
-  const int kq = L > 2048 ? 2 : (no_short ? 0 : (L <= 512 ? 8 : (L <= 1024 ? 16 : 0)));  // 2: some line past 2048
+  int short_n;
+  const int kq = split_kq(L, &short_n);
+  const SweepArgs SA = sweep_args(B, kplanes, ring, ldk, kstride, nb, kappa, thr_r, T_r, thr_stride, RT, mask_stride,
+                                  ld, short_n);
+  const ColsArgs CA = cols_args(B, kplanes, ldk, kstride, nb, kappa, RT, thr_c, T_c, thr_stride, maskT, mask_stride,
+                                ld, short_n);
   auto launch = [&](auto kqc) -> int {
     constexpr int KQ = decltype(kqc)::value;
     prof_begin(PH_SWEEP, s);
-    hipLaunchKernelGGL(k_sweep_rows9<KQ>, dim3(nstrips, nb), dim3(kThreads), 0, s, B, K, ldk, ldk, kstride, kappa,
-                       thr_r, T_r, thr_stride, RT, mask_stride, ld, short_n);
+    hipLaunchKernelGGL(k_sweep_rows9<KQ>, dim3(nstrips, nb), dim3(kThreads), 0, s, SA);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_SWEEP, s);
     prof_begin(PH_SEL_COLS, s);
-    hipLaunchKernelGGL(k_sel_cols9<KQ>, dim3((L + kColsPerBlock<KQ> - 1) / kColsPerBlock<KQ>, nb), dim3(256), 0, s, B, K,
-                       ldk, kstride, kappa, RT, thr_c, T_c, thr_stride, maskT, mask_stride, ld, short_n);
+    hipLaunchKernelGGL(k_sel_cols9<KQ>, dim3((L + kColsPerBlock<KQ> - 1) / kColsPerBlock<KQ>, nb), dim3(256), 0, s, CA);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_SEL_COLS, s);
+    return ACOSS_OK;
+  };
+  if (kq == 8) return launch(std::integral_constant<int, 8>{});
+  if (kq == 16) return launch(std::integral_constant<int, 16>{});
+  if (kq == 2) return launch(std::integral_constant<int, 2>{});
+  return launch(std::integral_constant<int, 0>{});
+}
+
+// One fused launch (k_sweep_cols9): the sweep + row select of sub-batch S (ns pairs, key planes
+// kpl_s, row words RT_s) and the column select of the previous sub-batch C (nc pairs, its planes
+// kpl_c and words RT_c, which an earlier launch on the same stream completed). Either may be empty.
+int launch_crp_split_fused(const SplitSide& S, const SplitSide& C, int L, float kappa, int ldk, int64_t kstride,
+                           int64_t thr_stride, int64_t mask_stride, int ld, hipStream_t s) {
+  if (S.B.m != kMS || S.B.tau != 1 || L > 4096) return 1;
+  const int nstrips = (L + kSR - 1) / kSR;
+  int short_n;
+  const int kq = split_kq(L, &short_n);
+  const SweepArgs SA = sweep_args(S.B, S.kpl, S.ring, ldk, kstride, S.nb > 0 ? S.nb : 1, kappa, S.thr_r, S.T_r,
+                                  thr_stride, S.RT, mask_stride, ld, short_n);
+  const ColsArgs CA = cols_args(C.B, C.kpl, ldk, kstride, C.nb > 0 ? C.nb : 1, kappa, C.RT, C.thr_c, C.T_c,
+                                thr_stride, C.maskT, mask_stride, ld, short_n);
+  auto launch = [&](auto kqc) -> int {
+    constexpr int KQ = decltype(kqc)::value;
+    const int ncb = (L + kColsPerBlock<KQ> - 1) / kColsPerBlock<KQ>;
+    const int nS = S.nb > 0 ? nstrips * S.nb : 0, nC = C.nb > 0 ? ncb * C.nb : 0;
+    const int blocks = 8 * (((nS + 7) >> 3) + ((nC + 7) >> 3));
+    if (blocks == 0) return ACOSS_OK;
+    hipLaunchKernelGGL(k_sweep_cols9<KQ>, dim3(blocks), dim3(kThreads), 0, s, SA, nstrips, nS, CA, ncb, nC);
+    ACOSS_LAUNCH_CHECK();
     return ACOSS_OK;
   };
   if (kq == 8) return launch(std::integral_constant<int, 8>{});
