@@ -26,12 +26,22 @@ def main():
     ap.add_argument("--blocks", type=int, default=446)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--seed", type=int, default=20250101)
+    ap.add_argument("--ar", type=float, default=0.0,
+                    help="AR(1) coefficient between consecutive blocks of a track (beat blocks overlap by "
+                         "blocksize - 1 beats, so real neighbours are close); 0 = independent rows")
     a = ap.parse_args()
     rng = np.random.Generator(np.random.PCG64(a.seed))
     NT, NB = a.tracks, a.blocks
-    mf = rng.standard_normal((NT * NB, 1000), dtype=np.float32)
-    ss = np.abs(rng.standard_normal((NT * NB, 1225), dtype=np.float32))
-    ch = np.abs(rng.standard_normal((NT * NB, 480), dtype=np.float32))
+
+    def feats(d):
+        x = rng.standard_normal((NT, NB, d), dtype=np.float32)
+        if a.ar > 0:
+            for i in range(1, NB):
+                x[:, i] = a.ar * x[:, i - 1] + np.float32(np.sqrt(1 - a.ar * a.ar)) * x[:, i]
+        return x.reshape(NT * NB, d)
+    mf = feats(1000)
+    ss = np.abs(feats(1225))
+    ch = np.abs(feats(480))
     med = np.abs(rng.standard_normal((NT, 12), dtype=np.float32))
     bank = {"mfccs": torch.as_tensor(mf).cuda(), "ssms": torch.as_tensor(ss).cuda(),
             "chromas": torch.as_tensor(ch).cuda(), "chroma_med": torch.as_tensor(med).cuda(),
