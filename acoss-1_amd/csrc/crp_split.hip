@@ -1562,13 +1562,15 @@ __global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(ColsArgs A) {
 // group counts (Bresenham), so both progress together through the launch.
 template <int KQ>
 __global__ __launch_bounds__(kThreads, ACOSS_SWEEP_WPE) void k_sweep_cols9(SweepArgs S, int nstrips, int nS,
-                                                                           ColsArgs C, int ncb, int nC) {
+                                                                           ColsArgs C, int ncb, int nC, int order) {
   __shared__ __attribute__((aligned(16))) char smem[kSweepLds<KQ> > (int)(4 * sizeof(WaveLds)) ? kSweepLds<KQ>
                                                                                                : (int)(4 * sizeof(WaveLds))];
   __shared__ int s_slot;
   const int gS = (nS + 7) >> 3, gC = (nC + 7) >> 3, gT = gS + gC;
   const int b = blockIdx.x, g = b >> 3, x = b & 7;
-  const int s0 = (int)(((int64_t)g * gS) / gT), s1 = (int)(((int64_t)(g + 1) * gS) / gT);
+  // order 0: interleaved in proportion; 1: the select groups first; 2: the sweep groups first
+  const int s0 = order == 0 ? (int)(((int64_t)g * gS) / gT) : order == 1 ? max(0, g - gC) : min(g, gS);
+  const int s1 = order == 0 ? (int)(((int64_t)(g + 1) * gS) / gT) : order == 1 ? max(0, g + 1 - gC) : min(g + 1, gS);
   if (s1 > s0) {  // a sweep group
     const int v = 8 * s0 + x;
     if (v < nS) sweep_rows_block<KQ>(S, v % nstrips, v / nstrips, smem, &s_slot);
@@ -1660,7 +1662,9 @@ int launch_crp_split_fused(const SplitSide& S, const SplitSide& C, int L, float 
     const int nS = S.nb > 0 ? nstrips * S.nb : 0, nC = C.nb > 0 ? ncb * C.nb : 0;
     const int blocks = 8 * (((nS + 7) >> 3) + ((nC + 7) >> 3));
     if (blocks == 0) return ACOSS_OK;
-    hipLaunchKernelGGL(k_sweep_cols9<KQ>, dim3(blocks), dim3(kThreads), 0, s, SA, nstrips, nS, CA, ncb, nC);
+    static const char* oenv = getenv("ACOSS_FUSED_ORDER");
+    const int order = oenv ? atoi(oenv) : 0;
+    hipLaunchKernelGGL(k_sweep_cols9<KQ>, dim3(blocks), dim3(kThreads), 0, s, SA, nstrips, nS, CA, ncb, nC, order);
     ACOSS_LAUNCH_CHECK();
     return ACOSS_OK;
   };
