@@ -679,11 +679,16 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   const size_t per_pair = 3 * mat * 4 + 4 * (size_t)wplane * 2 + 6 * (size_t)ld * 4 + 4 * sw_b + 4 * (4 + 4) + 4;
   size_t budget = (size_t)4 << 30;
   if (const char* e = getenv("ACOSS_EF_BYTES")) budget = strtoull(e, nullptr, 10);
-  int64_t chunk = (int64_t)(budget / per_pair);
+  // chunks alternate between two streams with a scratch set each, so one chunk's MFMA CSMs overlap
+  // the previous chunk's VALU/latency-bound binarize, k-smallest means and SW (one stream while
+  // phases are profiled, or with ACOSS_EF_STREAMS=1)
+  const char* st_env = getenv("ACOSS_EF_STREAMS");
+  const int nset = (profiling() || (st_env && st_env[0] == '1')) ? 1 : 2;
+  int64_t chunk = (int64_t)(budget / nset / per_pair);
   if (chunk < 1) chunk = 1;
   if (chunk > 65535) chunk = 65535;
   if (chunk > n_pairs) chunk = n_pairs;
-  char* ws = static_cast<char*>(workspace(11, per_pair * chunk + 16 * 256));
+  char* ws = static_cast<char*>(workspace(11, nset * (per_pair * chunk + 16 * 256)));
   if (!ws) return ACOSS_E_HIP;
   size_t o = 0;
   auto carve = [&](size_t bytes) {
@@ -691,23 +696,54 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
     o = align_up(o + bytes, 256);
     return r;
   };
-  float* C = reinterpret_cast<float*>(carve(3 * mat * 4 * chunk));
-  uint16_t* Wb = reinterpret_cast<uint16_t*>(carve(4 * (size_t)wplane * 2 * chunk));
-  float* rmean = reinterpret_cast<float*>(carve(3 * (size_t)ld * 4 * chunk));
-  float* cmean = reinterpret_cast<float*>(carve(3 * (size_t)ld * 4 * chunk));
-  void* bnd = carve(4 * sw_b * chunk);
-  int32_t* m_rows = reinterpret_cast<int32_t*>(carve(4 * 4 * chunk));
-  int32_t* m_cols = reinterpret_cast<int32_t*>(carve(4 * 4 * chunk));
-  int* oti = reinterpret_cast<int*>(carve(4 * chunk));
+  struct EfSet {
+    float* C;
+    uint16_t* Wb;
+    float *rmean, *cmean;
+    void* bnd;
+    int32_t *m_rows, *m_cols;
+    int* oti;
+  } sets[2];
+  for (int q = 0; q < nset; ++q) {
+    sets[q].C = reinterpret_cast<float*>(carve(3 * mat * 4 * chunk));
+    sets[q].Wb = reinterpret_cast<uint16_t*>(carve(4 * (size_t)wplane * 2 * chunk));
+    sets[q].rmean = reinterpret_cast<float*>(carve(3 * (size_t)ld * 4 * chunk));
+    sets[q].cmean = reinterpret_cast<float*>(carve(3 * (size_t)ld * 4 * chunk));
+    sets[q].bnd = carve(4 * sw_b * chunk);
+    sets[q].m_rows = reinterpret_cast<int32_t*>(carve(4 * 4 * chunk));
+    sets[q].m_cols = reinterpret_cast<int32_t*>(carve(4 * 4 * chunk));
+    sets[q].oti = reinterpret_cast<int*>(carve(4 * chunk));
+  }
+  hipStream_t ss[2] = {s, s};
+  if (nset == 2) {
+    ss[1] = side_stream(0);
+    if (!ss[1]) {
+      set_error("could not create the side stream");
+      return ACOSS_E_HIP;
+    }
+    hipEvent_t e0 = sync_event(0);  // the side stream starts after the per-track prep above
+    ACOSS_HIP_CHECK(hipEventRecord(e0, s));
+    ACOSS_HIP_CHECK(hipStreamWaitEvent(ss[1], e0, 0));
+  }
   const size_t bin_lds = (size_t)ld * 4;
   const int64_t mstride = (int64_t)mat * chunk;       // between the 3 CSM planes
   const int64_t meanstride = (int64_t)ld * chunk;     // between the 3 mean vectors
   const int tiles = (ld + kT - 1) / kT;
-  for (int64_t p0 = 0; p0 < n_pairs; p0 += chunk) {
+  int ci = 0;
+  for (int64_t p0 = 0; p0 < n_pairs; p0 += chunk, ++ci) {
     const int P = (int)((n_pairs - p0) < chunk ? (n_pairs - p0) : chunk);
     const EfPairs E{pairs + 2 * p0, block_off, n_blocks};
-    prof_begin(PH_CSM, s);
-    hipLaunchKernelGGL(k_ef_oti, dim3((P + 255) / 256), dim3(256), 0, s, chroma_med, pairs + 2 * p0, P, oti);
+    hipStream_t st = ss[ci & 1];
+    float* C = sets[ci & (nset - 1)].C;
+    uint16_t* Wb = sets[ci & (nset - 1)].Wb;
+    float* rmean = sets[ci & (nset - 1)].rmean;
+    float* cmean = sets[ci & (nset - 1)].cmean;
+    void* bnd = sets[ci & (nset - 1)].bnd;
+    int32_t* m_rows = sets[ci & (nset - 1)].m_rows;
+    int32_t* m_cols = sets[ci & (nset - 1)].m_cols;
+    int* oti = sets[ci & (nset - 1)].oti;
+    prof_begin(PH_CSM, st);
+    hipLaunchKernelGGL(k_ef_oti, dim3((P + 255) / 256), dim3(256), 0, st, chroma_med, pairs + 2 * p0, P, oti);
     ACOSS_LAUNCH_CHECK();
     {
       const int n_tiles = tiles * tiles * P;
@@ -717,10 +753,10 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
           d = (int)align_up((size_t)d, 4);
         }
         if (wave_tiles && d % 4 == 0)
-          hipLaunchKernelGGL(k_ef_csm_w<0>, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, s, bank, d, sq, E,
+          hipLaunchKernelGGL(k_ef_csm_w<0>, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, st, bank, d, sq, E,
                              oti, ld, n_tiles, dst);
         else
-          hipLaunchKernelGGL(k_ef_csm<0>, dim3((unsigned)n_tiles), dim3(256), 0, s, bank, d, sq, E, oti, ld, dst);
+          hipLaunchKernelGGL(k_ef_csm<0>, dim3((unsigned)n_tiles), dim3(256), 0, st, bank, d, sq, E, oti, ld, dst);
         ACOSS_LAUNCH_CHECK();
         return ACOSS_OK;
       };
@@ -728,56 +764,61 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
         return ACOSS_E_HIP;
     }
     if (wave_tiles && d_chroma % 24 == 0)
-      hipLaunchKernelGGL(k_ef_csm_w<1>, dim3((unsigned)((tiles * tiles * P + 3) / 4)), dim3(256), 0, s, chn, d_chroma,
+      hipLaunchKernelGGL(k_ef_csm_w<1>, dim3((unsigned)((tiles * tiles * P + 3) / 4)), dim3(256), 0, st, chn, d_chroma,
                          nullptr, E, oti, ld, tiles * tiles * P, C + 2 * mstride);
     else
-      hipLaunchKernelGGL(k_ef_csm<1>, dim3((unsigned)(tiles * tiles * P)), dim3(256), 0, s, chn, d_chroma, nullptr, E,
+      hipLaunchKernelGGL(k_ef_csm<1>, dim3((unsigned)(tiles * tiles * P)), dim3(256), 0, st, chn, d_chroma, nullptr, E,
                          oti, ld, C + 2 * mstride);
     ACOSS_LAUNCH_CHECK();
-    prof_end(PH_CSM, s);
-    prof_begin(PH_BIN, s);
-    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 3), dim3(1024), bin_lds, s, C, mstride, ld, E, kappa,
+    prof_end(PH_CSM, st);
+    prof_begin(PH_BIN, st);
+    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 3), dim3(1024), bin_lds, st, C, mstride, ld, E, kappa,
                        Wb, wplane, 0);
     ACOSS_LAUNCH_CHECK();
-    prof_end(PH_BIN, s);
-    prof_begin(PH_WCSM, s);
+    prof_end(PH_BIN, st);
+    prof_begin(PH_WCSM, st);
     if (K == 10) {  // EarlyFusion's K: the k-th smallest is a fixed register, no per-element select
-      hipLaunchKernelGGL((k_ef_kmin_rows<10, 10>), dim3((ld + 63) / 64, P, 3), dim3(64), 0, s, C, mstride, ld, E,
+      hipLaunchKernelGGL((k_ef_kmin_rows<10, 10>), dim3((ld + 63) / 64, P, 3), dim3(64), 0, st, C, mstride, ld, E,
                          (int)K, rmean, meanstride);
       ACOSS_LAUNCH_CHECK();
-      hipLaunchKernelGGL((k_ef_kmin<true, 10, 10>), dim3((ld + 255) / 256, P, 3), dim3(256), 0, s, C, mstride, ld,
+      hipLaunchKernelGGL((k_ef_kmin<true, 10, 10>), dim3((ld + 255) / 256, P, 3), dim3(256), 0, st, C, mstride, ld,
                          E, (int)K, cmean, meanstride);
       ACOSS_LAUNCH_CHECK();
     } else if (K <= kKmax) {
-      hipLaunchKernelGGL((k_ef_kmin_rows<kKmax>), dim3((ld + 63) / 64, P, 3), dim3(64), 0, s, C, mstride, ld, E,
+      hipLaunchKernelGGL((k_ef_kmin_rows<kKmax>), dim3((ld + 63) / 64, P, 3), dim3(64), 0, st, C, mstride, ld, E,
                          (int)K, rmean, meanstride);
       ACOSS_LAUNCH_CHECK();
-      hipLaunchKernelGGL((k_ef_kmin<true, kKmax>), dim3((ld + 255) / 256, P, 3), dim3(256), 0, s, C, mstride, ld, E,
+      hipLaunchKernelGGL((k_ef_kmin<true, kKmax>), dim3((ld + 255) / 256, P, 3), dim3(256), 0, st, C, mstride, ld, E,
                          (int)K, cmean, meanstride);
       ACOSS_LAUNCH_CHECK();
     } else {
-      hipLaunchKernelGGL(k_ef_kmean<false>, dim3((ld + 3) / 4, P, 3), dim3(256), 0, s, C, mstride, ld, E, (int)K,
+      hipLaunchKernelGGL(k_ef_kmean<false>, dim3((ld + 3) / 4, P, 3), dim3(256), 0, st, C, mstride, ld, E, (int)K,
                          rmean, meanstride);
       ACOSS_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_ef_kmean<true>, dim3((ld + 3) / 4, P, 3), dim3(256), 0, s, C, mstride, ld, E, (int)K,
+      hipLaunchKernelGGL(k_ef_kmean<true>, dim3((ld + 3) / 4, P, 3), dim3(256), 0, st, C, mstride, ld, E, (int)K,
                          cmean, meanstride);
       ACOSS_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_ef_wsum, dim3((unsigned)((mat + 255) / 256), P), dim3(256), 0, s, C, mstride, ld, E, rmean,
+    hipLaunchKernelGGL(k_ef_wsum, dim3((unsigned)((mat + 255) / 256), P), dim3(256), 0, st, C, mstride, ld, E, rmean,
                        cmean, meanstride, mu);
     ACOSS_LAUNCH_CHECK();
-    prof_end(PH_WCSM, s);
-    prof_begin(PH_BIN, s);
-    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 1), dim3(1024), bin_lds, s, C, mstride, ld, E, kappa,
+    prof_end(PH_WCSM, st);
+    prof_begin(PH_BIN, st);
+    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 1), dim3(1024), bin_lds, st, C, mstride, ld, E, kappa,
                        Wb, wplane, 3);
     ACOSS_LAUNCH_CHECK();
-    prof_end(PH_BIN, s);
-    prof_begin(PH_SW, s);
-    hipLaunchKernelGGL(k_ef_swmeta, dim3((P + 255) / 256), dim3(256), 0, s, E, P, m_rows, m_cols);
+    prof_end(PH_BIN, st);
+    prof_begin(PH_SW, st);
+    hipLaunchKernelGGL(k_ef_swmeta, dim3((P + 255) / 256), dim3(256), 0, st, E, P, m_rows, m_cols);
     ACOSS_LAUNCH_CHECK();
-    int rc = launch_swb_batch(Wb, wplane, ld, m_rows, m_cols, 4 * P, ld, ld, bnd, scores_out + 4 * p0, s);
+    int rc = launch_swb_batch(Wb, wplane, ld, m_rows, m_cols, 4 * P, ld, ld, bnd, scores_out + 4 * p0, st);
     if (rc) return rc;
-    prof_end(PH_SW, s);
+    prof_end(PH_SW, st);
+  }
+  if (nset == 2) {  // the caller's stream waits for the side stream's chunks
+    hipEvent_t e1 = sync_event(1);
+    ACOSS_HIP_CHECK(hipEventRecord(e1, ss[1]));
+    ACOSS_HIP_CHECK(hipStreamWaitEvent(s, e1, 0));
   }
   return ACOSS_OK;
 }
