@@ -485,6 +485,12 @@ def main():
                     "kernel_ms_sum_one_stream": round(kernel_ms_sum, 3) if kernel_ms_sum else None,
                     "dominant_kernel": dom, "kernels": kernels,
                     "valu_issue": valu}
+        if traffic:  # the same call against the HBM roofline of the bytes it actually moves
+            bpp = traffic / batch_pairs
+            bound = 8e12 / bpp
+            roofline["hbm_traffic"] = {"bytes_per_pair": round(bpp), "algorithmic_bytes_per_pair": 4 * 12 * 2 * args.frames,
+                                       "pairs_per_s_at_8TBps": round(bound, 1),
+                                       "frac": round(batch_pairs / (launch_ms * 1e-3) / bound, 4)}
 
         map_parity, cpu = None, None
         if world == 1 and args.corpus == "hard":
