@@ -1662,7 +1662,7 @@ int launch_crp_split_fused(const SplitSide& S, const SplitSide& C, int L, float 
     const int nS = S.nb > 0 ? nstrips * S.nb : 0, nC = C.nb > 0 ? ncb * C.nb : 0;
     const int blocks = 8 * (((nS + 7) >> 3) + ((nC + 7) >> 3));
     if (blocks == 0) return ACOSS_OK;
-    static const char* oenv = getenv("ACOSS_FUSED_ORDER");
+    const char* oenv = getenv("ACOSS_FUSED_ORDER");
     const int order = oenv ? atoi(oenv) : 0;
     hipLaunchKernelGGL(k_sweep_cols9<KQ>, dim3(blocks), dim3(kThreads), 0, s, SA, nstrips, nS, CA, ncb, nC, order);
     ACOSS_LAUNCH_CHECK();

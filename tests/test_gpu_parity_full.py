@@ -74,9 +74,12 @@ def test_full_corpus_qmax_and_map_parity_500():
     {"ACOSS_KEY_BYTES": str(20 << 20)},                           # ~2 pairs per key-plane sub-batch
     {"ACOSS_SPLIT_STREAMS": "3", "ACOSS_KEY_BYTES": str(40 << 20)},
     {"ACOSS_BATCH_PAIRS": "5", "ACOSS_SPLIT_STREAMS": "1", "ACOSS_KEY_BYTES": "1"},  # 1 pair per sub-batch
-    {"ACOSS_SPLIT_FUSED": "0"},                                   # two streams instead of fused launches
+    {"ACOSS_SPLIT_FUSED": "0"},                                   # two streams of separate kernels
     {"ACOSS_SPLIT_FUSED": "0", "ACOSS_KEY_BYTES": str(20 << 20)},
-    {"ACOSS_KEY_BYTES": "1"},                                     # fused launches of 1 + 1 pairs
+    {"ACOSS_SPLIT_FUSED": "1"},                                   # fused launches (auto: lines > 1536 only)
+    {"ACOSS_SPLIT_FUSED": "1", "ACOSS_KEY_BYTES": str(20 << 20)},
+    {"ACOSS_SPLIT_FUSED": "1", "ACOSS_KEY_BYTES": "1"},           # fused launches of 1 + 1 pairs
+    {"ACOSS_SPLIT_FUSED": "1", "ACOSS_FUSED_ORDER": "1"},         # block order is free (A/B knob)
 ])
 def test_batching_branches_ragged(monkeypatch, env):
     from acoss.engine import ChromaBank
