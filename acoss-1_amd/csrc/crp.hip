@@ -1204,15 +1204,12 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
     const int v = e ? atoi(e) : 2;
     return v < 1 ? 1 : (v > 3 ? 3 : v);
   }();
-  // fused launches (k_sweep_cols9: a sub-batch's sweep and the previous one's column select in one
-  // grid, on the caller's stream) replace the side streams unless ACOSS_SPLIT_FUSED=0; they need
-  // the two plane buffers of the two-stream mode
-  // (auto: launches with lines past 1536 codes; measured 82.2k vs 81.3k pairs/s at 2000 frames,
-  // but separate kernels ran faster for shorter and mixed lengths: 718k vs 608k at 500 frames,
-  // 231k vs 229k at 1000, 289k vs 275k for U[250, 1250])
+  // fused launches (k_sweep_cols9: a sub-batch's sweep and an earlier one's column select in one
+  // grid) instead of separate kernels: opt-in, ACOSS_SPLIT_FUSED=1 (with >= 2 streams; measured 82.2k vs 81.3k pairs/s at exactly 2000 frames, but
+  // separate kernels ran faster at every other shape tried: 718k vs 608k at 500 frames, 231k vs
+  // 229k at 1000, 289k vs 275k for U[250, 1250], 71.8k vs 70.9k for U[1800, 2200])
   const char* fused_env = getenv("ACOSS_SPLIT_FUSED");
-  const bool fused = split && nbuf >= 2 &&
-                     (fused_env ? fused_env[0] == '1' : L > 1536);
+  const bool fused = split && nbuf >= 2 && fused_env && fused_env[0] == '1';
   // fused launches alternate between two streams, launch k pairing sub-batch k's sweep with
   // sub-batch k-2's select (same stream): four plane buffers keep every writer and reader apart
   const int nkb = fused ? 4 : nbuf;

@@ -412,8 +412,8 @@ def main():
     value = total_pairs * args.steps / dt
 
     # ---- one call of the path timed with HIP events on the stream it is launched on ----
-    # (a) as the timed steps run it (fused launches of one sub-batch's sweep with an earlier one's
-    #     column select, alternating two streams) -> roofline.achieved; (b) with ACOSS_SPLIT_STREAMS=1 and the library's per-phase
+    # (a) as the timed steps run it (two streams: one sub-batch's selects overlap the next one's
+    #     sweep) -> roofline.achieved; (b) with ACOSS_SPLIT_STREAMS=1 and the library's per-phase
     #     events, so the kernel durations add up to that call's time -> roofline.kernels
     phases = {}
     call_ms = call1_ms = None
@@ -479,7 +479,7 @@ def main():
         roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": traffic,
                     "kernel": "acoss_crp_align (one call = oti + sweep/select_rows + select_cols + dp_qmax on "
-                              "%d pairs; fused sweep/select launches of key-plane sub-batches on two streams)" % batch_pairs,
+                              "%d pairs; key-plane sub-batches on two streams)" % batch_pairs,
                     "ops_per_pair": opp, "ops_split_per_pair": split, "launch_ms": round(launch_ms, 3),
                     "one_stream_call_ms": round(call1_ms, 3) if call1_ms else None,
                     "kernel_ms_sum_one_stream": round(kernel_ms_sum, 3) if kernel_ms_sum else None,
