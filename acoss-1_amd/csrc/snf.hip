@@ -198,7 +198,7 @@ template <bool TRANS>
 int snf_spmm(const double* D, int64_t ldd, int32_t dcols, int32_t nout, int32_t row0, int32_t K, const int32_t* Js,
              const double* Vs, double reg_diag, double* out, int64_t ldo, hipStream_t s) {
   const int32_t rblocks = (nout + kSnfRB - 1) / kSnfRB, nchunks = (dcols + kSnfW - 1) / kSnfW;
-  static const char* vwenv = getenv("ACOSS_SNF_VW");
+  const char* vwenv = getenv("ACOSS_SNF_VW");
   const bool even = ldd % 2 == 0 && dcols % 2 == 0 && (TRANS || ldo % 2 == 0);
   const bool v2 = even && !(vwenv && vwenv[0] == '1');
   auto kern = v2 ? k_snf_spmm<TRANS, 2> : k_snf_spmm<TRANS, 1>;

@@ -180,11 +180,14 @@ def test_earlyfusion_composition(tmp_path, monkeypatch):
     _assert_snf_close(np.asarray(ef.Ds["early+late"]), ref_el)
 
 
-@pytest.mark.parametrize("n,K,L", [(40, 5, 2), (333, 20, 3), (1030, 7, 4)])
-def test_snf_step_bitexact(n, K, L):
+@pytest.mark.parametrize("n,K,L,vw", [(40, 5, 2, None), (333, 20, 3, None), (1030, 7, 4, None), (1030, 7, 2, "1")])
+def test_snf_step_bitexact(monkeypatch, n, K, L, vw):
     """acoss_snf_step vs the reference's own scipy expression (np_oracle.snf_step): the HIP
-    kernels sum in csr column order with unfused multiply/add, so the result is bit-exact."""
+    kernels sum in csr column order with unfused multiply/add, so the result is bit-exact.
+    Even n gathers two columns per lane (16-byte loads), odd n one; vw = "1" forces one."""
     import torch
+    if vw:
+        monkeypatch.setenv("ACOSS_SNF_VW", vw)
     rng = np.random.default_rng(n)
     mats = [rng.random((n, n)) for _ in range(L)]
     J = np.stack([rng.choice(n, K, replace=False) for _ in range(n)]).astype(np.int32)
