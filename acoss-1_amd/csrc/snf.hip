@@ -199,7 +199,8 @@ int snf_spmm(const double* D, int64_t ldd, int32_t dcols, int32_t nout, int32_t 
              const double* Vs, double reg_diag, double* out, int64_t ldo, hipStream_t s) {
   const int32_t rblocks = (nout + kSnfRB - 1) / kSnfRB, nchunks = (dcols + kSnfW - 1) / kSnfW;
   const char* vwenv = getenv("ACOSS_SNF_VW");
-  const bool even = ldd % 2 == 0 && dcols % 2 == 0 && (TRANS || ldo % 2 == 0);
+  const bool even = ldd % 2 == 0 && dcols % 2 == 0 && reinterpret_cast<uintptr_t>(D) % 16 == 0 &&
+                    (TRANS || (ldo % 2 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0));
   const bool v2 = even && !(vwenv && vwenv[0] == '1');
   auto kern = v2 ? k_snf_spmm<TRANS, 2> : k_snf_spmm<TRANS, 1>;
   hipLaunchKernelGGL(kern, dim3((unsigned)rblocks * (unsigned)nchunks), dim3(256), 0, s, D, ldd, dcols, nout, row0, K,
