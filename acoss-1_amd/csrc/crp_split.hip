@@ -791,6 +791,7 @@ __device__ __forceinline__ unsigned prefix_of_rank(const LT& L, int rho, unsigne
   // unrolled SWAR body once): 0 hint, 1 gallop down, 2 gallop up, 3 bisect
   int mode = (hint != kNoHint) ? 0 : 3;
   unsigned step = 1;
+#ifdef ACOSS_SEARCH_BRANCHY
   while (a < b) {
     unsigned t;
     if (mode == 0)
@@ -818,6 +819,32 @@ __device__ __forceinline__ unsigned prefix_of_rank(const LT& L, int rho, unsigne
     else if (mode == 2)
       mode = greater ? 3 : (step <<= 1, 2);
   }
+#else
+  // The same search with its control kept in integer arithmetic on wave-uniform values (the
+  // compare result as a 0/1 int from the sign of rho - c, the mode transitions and step doublings
+  // as 2-bit / 1-bit table lookups): no per-pass branches and no bool round trip through a VGPR.
+  // mode' = T[2 mode + g] (2 bits each): (0,0)->2 (0,1)->1 (1,0)->3 (1,1)->1 (2,0)->2 (2,1)->3 (3,*)->3
+  constexpr unsigned kNext = (2u << 0) | (1u << 2) | (3u << 4) | (1u << 6) | (2u << 8) | (3u << 10) | (3u << 12) |
+                             (3u << 14);
+  constexpr unsigned kDouble = (1u << 3) | (1u << 4);  // gallop continues: (1, greater), (2, not greater)
+  while (a < b) {
+    const unsigned w = b - a, mid = (a + b) >> 1;
+    const unsigned th = hint < a ? a : (hint > b ? b : hint);
+    const unsigned tdown = w > step ? b - step : a;
+    const unsigned tup = w > step ? a + step - 1 : mid;
+    const unsigned t = mode == 0 ? th : (mode == 1 ? tdown : (mode == 2 ? tup : mid));
+    const int c = L.count_le(t);
+    ++*passes;
+    const unsigned g = (unsigned)(rho - c) >> 31;  // 1 iff c > rho
+    b = g ? t : b;
+    c_b = g ? c : c_b;
+    a = g ? a : t + 1;
+    c_am1 = g ? c_am1 : c;
+    const unsigned idx = 2u * (unsigned)mode + g;
+    step <<= (kDouble >> idx) & 1u;
+    mode = (int)((kNext >> (2u * idx)) & 3u);
+  }
+#endif
   *le_out = c_b;
   *less_out = c_am1;
   return a;
