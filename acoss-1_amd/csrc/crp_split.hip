@@ -865,7 +865,8 @@ template <class LT>
 __device__ __forceinline__ unsigned sample_hint(const LT& L, int n, float kappa) {
   const unsigned v = L.sample();  // kNone on lanes whose sample is past the line
   const int ns = __popcll(__ballot(v != kNone));
-  const int k = (int)((float)(n - 1) * kappa * (float)ns / (float)n);
+  // (a guess only: the hardware reciprocal instead of an IEEE division sequence)
+  const int k = (int)((float)(n - 1) * kappa * (float)ns * __builtin_amdgcn_rcpf((float)n));
   // the k-th smallest sample: the least P with #(samples <= P) > k, by bisection over the
   // samples' range with one ballot per step (no DPP chains)
   unsigned lo = wave_min_u32(v), hi = wave_max_u32(v != kNone ? v : 0u);
