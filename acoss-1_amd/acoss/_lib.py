@@ -52,7 +52,7 @@ SIGNATURES = {
     "acoss_simple_features": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _i64, _vp],
     "acoss_earlyfusion": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, ctypes.c_double,
                           _i32, _f32, _vp, _vp],
-    "acoss_ef_block_features": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp,
+    "acoss_ef_block_features": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp,
                                 _vp, _vp],
     "acoss_ds_finish": [_vp, _i32, _i64, _vp, _i32, _i32, _vp, _vp],
     "acoss_eval_ranks": [_vp, _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp],
@@ -511,10 +511,13 @@ def earlyfusion(bank, pairs, kappa=0.1, K=10, mu=0.5):
 
 def ef_block_features(chromas, mfccs, onsets, blocksize=20, mfccs_per_block=50, chromas_per_block=40):
     """EarlyFusion block features of a batch of tracks on the device (acoss_ef_block_features).
-    chromas: list of (n_t, 12); mfccs: list of (n_t, d) frame-major (mfcc_htk.T); onsets: list of
-    frame-index arrays. NaN MFCCs become 0 (earlyfusion_traile.py:98). Returns a dict of device
-    tensors 'mfccs' (B, R*d), 'ssms' (B, R(R-1)/2), 'chromas' (B, Rc*12), 'chroma_med' (T, 12)
-    and host 'block_off' (T,) int64 / 'n_blocks' (T,) int32 (blocks of track t: rows
+    chromas: list of (n_t, 12); mfccs: list of (m_t, d) frame-major (mfcc_htk.T; m_t may differ from
+    n_t: the extractor's MFCC frames are longer, features.py:884); onsets: list of frame-index arrays.
+    Block b spans mfcc[o[b]:o[b+blocksize-1]] and chroma[o[b]:o[b+blocksize]], each clamped to its
+    own length as the reference's slicing (resize_block, earlyfusion_traile.py:240); an empty span
+    raises ValueError, as the reference's resize does. NaN MFCCs become 0 (:98). Returns a dict of
+    device tensors 'mfccs' (B, R*d), 'ssms' (B, R(R-1)/2), 'chromas' (B, Rc*12), 'chroma_med'
+    (T, 12) and host 'block_off' (T,) int64 / 'n_blocks' (T,) int32 (blocks of track t: rows
     block_off[t] .. + n_blocks[t])."""
     torch = _torch()
     lib = load_library()
@@ -522,21 +525,33 @@ def ef_block_features(chromas, mfccs, onsets, blocksize=20, mfccs_per_block=50, 
     if not (len(mfccs) == len(onsets) == T):
         raise ValueError("one chroma, mfcc and onset array per track")
     n = np.array([len(c) for c in chromas], np.int64)
+    nm = np.array([len(m) for m in mfccs], np.int64)
     d = int(np.asarray(mfccs[0]).shape[1]) if T else 20
     nb = np.zeros(T, np.int64)
     for t in range(T):
         o = np.asarray(onsets[t], np.int64)
-        if np.asarray(mfccs[t]).shape != (n[t], d):
-            raise ValueError("track %d: mfcc must be (n_frames, %d) like its chroma" % (t, d))
+        if np.asarray(mfccs[t]).ndim != 2 or np.asarray(mfccs[t]).shape[1] != d:
+            raise ValueError("track %d: mfcc must be (n_frames, %d) like the first track's" % (t, d))
         if len(o) < blocksize:  # the reference's np.zeros((n_beats - blocksize, ...)) raises here (:106)
             raise ValueError("track %d: %d beats, fewer than blocksize=%d (negative dimensions are not allowed)"
                              % (t, len(o), blocksize))
         nb[t] = len(o) - blocksize
         if nb[t]:
-            if o.min() < 0 or o.max() > n[t] or np.any(np.diff(o) <= 0):
-                raise ValueError("track %d: onsets must increase inside the track" % t)
+            if o.min() < 0:
+                raise ValueError("track %d: negative onset frame" % t)
+            b = np.arange(nb[t])
+            # the clamped spans of every block (Python slicing); the reference's resize raises on
+            # an empty one (skimage.transform.resize of a (0, d) block)
+            m1, m2 = np.minimum(o[b], nm[t]), np.minimum(o[b + blocksize - 1], nm[t])
+            c1, c2 = np.minimum(o[b], n[t]), np.minimum(o[b + blocksize], n[t])
+            if np.any(m2 <= m1) or np.any(c2 <= c1):
+                bad = int(np.flatnonzero((m2 <= m1) | (c2 <= c1))[0])
+                raise ValueError("track %d: beat block %d spans no frames (onsets %d..%d, %d chroma / %d mfcc "
+                                 "frames)" % (t, bad, o[bad], o[bad + blocksize], n[t], nm[t]))
     foff = np.zeros(T, np.int64)
     foff[1:] = np.cumsum(n[:-1])
+    moff = np.zeros(T, np.int64)
+    moff[1:] = np.cumsum(nm[:-1])
     ooff = np.zeros(T, np.int64)
     ooff[1:] = np.cumsum([len(o) for o in onsets][:-1])
     boff = np.zeros(T, np.int64)
@@ -548,15 +563,17 @@ def ef_block_features(chromas, mfccs, onsets, blocksize=20, mfccs_per_block=50, 
     on = np.concatenate([np.asarray(o, np.int64) for o in onsets]) if T else np.zeros(0, np.int64)
     d_mf, d_ch = _dev(mf, torch.float32), _dev(ch, torch.float32)
     d_foff, d_n = _dev(foff, torch.int64), _dev(n.astype(np.int32), torch.int32)
+    d_moff, d_nm = _dev(moff, torch.int64), _dev(nm.astype(np.int32), torch.int32)
     d_on, d_ooff, d_boff = _dev(on, torch.int64), _dev(ooff, torch.int64), _dev(boff, torch.int64)
     R, Rc = int(mfccs_per_block), int(chromas_per_block)
     out = {"mfccs": torch.empty((B, R * d), dtype=torch.float32, device="cuda"),
            "ssms": torch.empty((B, R * (R - 1) // 2), dtype=torch.float32, device="cuda"),
            "chromas": torch.empty((B, Rc * 12), dtype=torch.float32, device="cuda"),
            "chroma_med": torch.empty((T, 12), dtype=torch.float32, device="cuda")}
-    rc = lib.acoss_ef_block_features(_ptr(d_mf), _ptr(d_ch), _ptr(d_foff), _ptr(d_n), _ptr(d_on), _ptr(d_ooff),
-                                     _ptr(d_boff), T, B, int(blocksize), R, Rc, d, _ptr(out["mfccs"]),
-                                     _ptr(out["ssms"]), _ptr(out["chromas"]), _ptr(out["chroma_med"]), _stream())
+    rc = lib.acoss_ef_block_features(_ptr(d_mf), _ptr(d_ch), _ptr(d_foff), _ptr(d_n), _ptr(d_moff), _ptr(d_nm),
+                                     _ptr(d_on), _ptr(d_ooff), _ptr(d_boff), T, B, int(blocksize), R, Rc, d,
+                                     _ptr(out["mfccs"]), _ptr(out["ssms"]), _ptr(out["chromas"]),
+                                     _ptr(out["chroma_med"]), _stream())
     _check(rc, "acoss_ef_block_features")
     out["block_off"] = boff
     out["n_blocks"] = nb.astype(np.int32)

@@ -18,8 +18,8 @@ What changes is how the pair loop runs (algorithm_template.py:142-193). The refe
     all-gather, `Ds += Ds.T` and the subclasses' normalize_by_length run as HIP kernels
     (finish.hip), and getEvalStatistics ranks on the device (acoss_eval_ranks), so no O(N^2)
     host loop is left for Da-TACOS-sized runs (SURVEY.md §8f row 1);
-  * only rank 0 keeps the file-backed memmap and writes the results (other ranks hold Ds in
-    memory), so ranks never write the same file;
+  * every rank keeps Ds in a file-backed memmap of its own (rank 0: the reference's file, other
+    ranks '<file>.rank<r>'), and only rank 0 writes the results, so ranks never write one file;
   * Ds is saved as '<prefix>_Ds.h5' (the reference's file, :163,193; one dataset per
     similarity type, as deepdish lays out a dict) when h5py is importable, and always as the
     '<prefix>_Ds.npz' twin; `precomputed=True` reads either back.
@@ -72,17 +72,20 @@ class CoverAlgorithm(object):
         self.Ds = {}
         _, rank = _dist_info()
         for s in similarity_types:
-            if rank == 0:
-                self.Ds[s] = np.memmap("%s_%s_dmat" % (self.get_cacheprefix(), s), shape=(self.N, self.N),
-                                       mode="w+", dtype="float32")
-            else:
-                self.Ds[s] = np.zeros((self.N, self.N), np.float32)
+            self.Ds[s] = np.memmap(self._dmat_path(s, rank), shape=(self.N, self.N), mode="w+", dtype="float32")
         self._prepared = False
         print("Initialized %s algorithm on %i songs in dataset %s" % (name, self.N, shortname))
 
     # ------------------------------------------------------------------ features
     def get_cacheprefix(self):
         return "%s/%s_%s" % (self.cachedir, self.name, self.shortname)
+
+    def _dmat_path(self, s, rank=0):
+        """The memmap file of Ds[s] (:61). Ranks other than 0 keep their copy of the assembled
+        matrix in a file of their own ('.rank<r>'), so no two ranks write one file and no rank
+        holds N x N float32 per similarity type in RAM (0.9 GB each at Da-TACOS size)."""
+        base = "%s_%s_dmat" % (self.get_cacheprefix(), s)
+        return base if rank == 0 else "%s.rank%d" % (base, rank)
 
     def load_features(self, i):
         """Feature dict of song i; records its clique as a side effect (:70-94)."""
@@ -157,10 +160,9 @@ class CoverAlgorithm(object):
         else:
             bounds = [(0, self.N)]
         r0, r1 = bounds[rank]
-        pairs = _dist.stripe_pairs(self.N, r0, r1, symmetric)
-        if not self._device_all_pairwise(pairs, bounds, r0, r1, world, symmetric):
-            for c0 in range(0, len(pairs), PAIR_CHUNK):
-                self.similarity(pairs[c0:c0 + PAIR_CHUNK])
+        if not self._device_all_pairwise(bounds, r0, r1, world, symmetric):
+            for chunk in self._pair_chunks(r0, r1, symmetric):
+                self.similarity(chunk)
             if world > 1:
                 self._gather_stripes(bounds, r0, r1)
             if symmetric:
@@ -169,7 +171,24 @@ class CoverAlgorithm(object):
         if rank == 0:
             self._save_Ds(prefix)
 
-    def _device_all_pairwise(self, pairs, bounds, r0, r1, world, symmetric):
+    def _pair_chunks(self, r0, r1, symmetric):
+        """The stripe's pairs in the reference's enumeration order (combinations / permutations,
+        :168-171), PAIR_CHUNK at a time, with a progress line on stderr about every 10 s (the
+        reference prints progress in its serial loop, :179-187)."""
+        import sys
+        import time
+        n_pairs = sum(self.N - i - 1 if symmetric else self.N - 1 for i in range(r0, r1))
+        t0 = last = time.perf_counter()
+        done = 0
+        for chunk in _dist.stripe_pair_chunks(self.N, r0, r1, symmetric, PAIR_CHUNK):
+            yield chunk
+            done += len(chunk)
+            now = time.perf_counter()
+            if now - last >= 10.0 and done < n_pairs:
+                last = now
+                print("%s: %d / %d pairs, %.1f s" % (self.name, done, n_pairs, now - t0), file=sys.stderr, flush=True)
+
+    def _device_all_pairwise(self, bounds, r0, r1, world, symmetric):
         """The pair loop with the stripe kept in HBM: score chunks on the device, scatter into
         the (r1 - r0, N) stripe, one all-gather (world > 1), symmetrise with acoss_ds_finish,
         one copy into Ds. Returns False if the subclass has no device scorer."""
@@ -178,17 +197,19 @@ class CoverAlgorithm(object):
         import torch
         from .. import _lib
         blocks = {k: torch.zeros((r1 - r0, self.N), dtype=torch.float32, device="cuda") for k in self.Ds}
-        for c0 in range(0, len(pairs), PAIR_CHUNK):
-            chunk = pairs[c0:c0 + PAIR_CHUNK]
+        for chunk in self._pair_chunks(r0, r1, symmetric):
             sc = self._device_scores(chunk)
             p = torch.as_tensor(np.asarray(chunk, np.int64)).cuda()
             for k in blocks:
                 blocks[k][p[:, 0] - r0, p[:, 1]] = sc[k]
-        for k, blk in blocks.items():
+        for k in list(blocks):
+            blk = blocks.pop(k)
             full = _dist.all_gather_stripes(blk, bounds) if world > 1 else blk
+            del blk
             if symmetric:
                 _lib.ds_finish(full, symmetric=True)
             self.Ds[k][:] = full.cpu().numpy()
+            del full  # one assembled matrix on the device at a time
         return True
 
     def _gather_stripes(self, bounds, r0, r1):
@@ -238,8 +259,9 @@ class CoverAlgorithm(object):
 
     def cleanup_memmap(self):
         """Delete the memmap files of Ds (:195-203)."""
+        _, rank = _dist_info()
         for s in list(self.Ds):
-            path = "%s_%s_dmat" % (self.get_cacheprefix(), s)
+            path = self._dmat_path(s, rank)
             try:
                 if os.path.exists(path):
                     os.remove(path)

@@ -175,6 +175,23 @@ class EarlyFusion(CoverAlgorithm):
         for s, key in enumerate(("mfccs", "ssms", "chromas", "early")):
             self.Ds[key][idxs[:, 0], idxs[:, 1]] = scores[:, s]
 
+    def _device_scores(self, idxs):
+        """The four scores of every pair as float32 device tensors (the memmap's dtype), from one
+        acoss_earlyfusion call: all_pairwise keeps the stripe on the device and all-gathers it
+        across ranks (algorithm_template._device_all_pairwise)."""
+        idxs = np.asarray(idxs)
+        tic = time.time()
+        sc = _lib.earlyfusion(self._bank(), idxs.astype(np.int32), self.kappa, self.K)
+        if self.log_times:
+            self.times['raw'].append((time.time() - tic) / max(1, len(idxs)))
+        return {key: sc[:, s].float() for s, key in enumerate(("mfccs", "ssms", "chromas", "early"))}
+
+    def track_lengths(self):
+        """Beat blocks per song: a pair costs nb_i * nb_j (three CSMs, four SW), so the row
+        stripes balance that (acoss.distributed.stripe_bounds with m = tau = 0)."""
+        self.prepare()
+        return np.array([max(1, self.all_block_feats[i]["mfccs"].shape[0]) for i in range(self.N)], np.int64)
+
     def prepare(self, chunk=256):
         """Every song's block features: from the memory / disk cache, the rest on the GPU in
         batches of `chunk` songs."""

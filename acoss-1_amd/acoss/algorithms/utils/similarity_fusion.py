@@ -152,7 +152,9 @@ def _fusion_ws(Ws, K=5, niters=20, reg_diag=1):
         _lib.check_knn(Jt, Pts[0].shape[0])
     world, rank = _shard_world()
     if world > 1 and Pts[0].shape[0] >= world:  # (fewer rows than ranks: every rank runs it whole)
-        return _fusion_sharded(Pts, Js, Vs, niters, reg_diag, world, rank)
+        plan = shard_plan(Pts, Js, Vs, reg_diag, world, rank)
+        if plan["shard"]:
+            return _fusion_sharded(Pts, Js, Vs, niters, reg_diag, world, rank)
     for it in range(niters):
         # the reference's `Pts = nextPts` aliasing: from the second iteration on, matrix i's
         # update already sees the new matrices k < i; replacing Pts[i] in place of the list
@@ -168,15 +170,72 @@ def _fusion_ws(Ws, K=5, niters=20, reg_diag=1):
 
 
 def _shard_world():
-    """(world, rank) when the fusion should row-shard across torch.distributed ranks, else
-    (1, 0). ACOSS_SNF_SHARD=0 keeps every rank on the whole matrices (replicated)."""
+    """(world, rank) of the torch.distributed job when the fusion may row-shard across its ranks,
+    else (1, 0). ACOSS_SNF_SHARD=0 keeps every rank on the whole matrices (replicated)."""
     import os
     import torch.distributed as dist
-    if os.environ.get("ACOSS_SNF_SHARD", "1") == "0":
+    if os.environ.get("ACOSS_SNF_SHARD", "auto") == "0":
         return 1, 0
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         return dist.get_world_size(), dist.get_rank()
     return 1, 0
+
+
+# the last sharding decision (shard_plan), for logs and the bench line
+LAST_PLAN = {}
+
+
+def shard_plan(Pts, Js, Vs, reg_diag, world, rank, force=None):
+    """Decide row-sharded vs replicated cross-diffusion by measurement, the same way on every rank.
+
+    A replicated step for one matrix costs t_rep on every rank. Sharded, a rank computes its 1/W
+    of the rows of both halves (about t_rep / W) and waits for ONE all-gather of B (n x n float64,
+    the exchange) per step. Both grow as n^2, so the choice depends on the exchange bandwidth
+    against HBM, not on n: sharding pays when t_gather < t_rep (1 - 1/W). This times one
+    replicated step (result discarded) and one all-gather of B-sized stripes, takes the maximum
+    over ranks, and shards when t_gather <= 0.8 t_rep (1 - 1/W) (20 % margin for the per-step
+    launch and synchronisation costs the estimate leaves out). ACOSS_SNF_SHARD=1 forces sharding
+    (force=True), =0 never reaches here; the default is this rule ("auto")."""
+    import os
+    import time
+    import torch.distributed as dist
+    from ... import distributed as _dist
+    torch = _lib._torch()
+    mode = os.environ.get("ACOSS_SNF_SHARD", "auto")
+    if force is None and mode == "1":
+        force = True
+    n = int(Pts[0].shape[0])
+    bounds = shard_rows(n, world)
+    r0, r1 = bounds[rank]
+
+    def sync():
+        if Pts[0].is_cuda:
+            torch.cuda.synchronize()
+    sync()
+    t0 = time.perf_counter()
+    _lib.snf_step(Pts, 0, Js[0], Vs[0], reg_diag, validated=True)
+    sync()
+    t_rep = time.perf_counter() - t0
+    Bs = torch.zeros((r1 - r0, n), dtype=torch.float64, device=Pts[0].device)
+    dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    B = _dist.all_gather_stripes(Bs, bounds)
+    sync()
+    t_gather = time.perf_counter() - t0
+    del B, Bs
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor([t_rep, t_gather], dtype=torch.float64, device="cuda" if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_rep, t_gather = float(t[0]), float(t[1])
+    rule = t_gather <= 0.8 * t_rep * (1.0 - 1.0 / world)
+    shard = bool(force) if force is not None else rule
+    LAST_PLAN.clear()
+    LAST_PLAN.update({"n": n, "world": world, "backend": dist.get_backend(), "mode": mode,
+                      "t_step_replicated_ms": round(t_rep * 1e3, 3), "t_gather_B_ms": round(t_gather * 1e3, 3),
+                      "gather_GBps": round(8.0 * n * n * (world - 1) / world / max(t_gather, 1e-9) / 1e9, 1),
+                      "rule_shard": bool(rule), "shard": shard})
+    return dict(LAST_PLAN)
 
 
 def shard_rows(n, world):

@@ -42,8 +42,9 @@ def benchmark(dataset_csv, feature_dir, feature_type="hpcp", algorithm="Serra09"
     elif algorithm in ("EarlyFusionTraile", "EarlyFusion"):
         from .algorithms.earlyfusion_traile import EarlyFusion
         algo = EarlyFusion(**kw)
-        for i in range(len(algo.filepaths)):
-            algo.load_features(i)
+        # the reference's load_features(i) loop (coverid.py:80-81): the same per-song caches and clique
+        # bookkeeping, with the uncached songs' block features made ceil(N / 256) launches at a time
+        algo.prepare()
         logger.info('Feature loading done...')
         logger.info('Computing pairwise similarity...')
         algo.all_pairwise(parallel, n_cores=n_workers, symmetric=True)

@@ -51,6 +51,29 @@ def stripe_pairs(n, r0, r1, symmetric=True):
     return np.concatenate(out).astype(np.int32) if out else np.zeros((0, 2), np.int32)
 
 
+def stripe_pair_chunks(n, r0, r1, symmetric=True, chunk=1 << 20):
+    """The pairs of stripe_pairs(n, r0, r1, symmetric), same order, as (<= chunk, 2) int32 arrays,
+    formed one chunk at a time (a Da-TACOS stripe holds 10^8 pairs: never materialised whole)."""
+    buf, have = [], 0
+    for i in range(r0, r1):
+        js = np.arange(i + 1, n, dtype=np.int32) if symmetric else \
+            np.concatenate([np.arange(0, i, dtype=np.int32), np.arange(i + 1, n, dtype=np.int32)])
+        pos = 0
+        while pos < len(js):
+            take = min(chunk - have, len(js) - pos)
+            part = np.empty((take, 2), np.int32)
+            part[:, 0] = i
+            part[:, 1] = js[pos:pos + take]
+            buf.append(part)
+            have += take
+            pos += take
+            if have == chunk:
+                yield np.concatenate(buf) if len(buf) > 1 else buf[0]
+                buf, have = [], 0
+    if have:
+        yield np.concatenate(buf) if len(buf) > 1 else buf[0]
+
+
 def scatter_stripe(pairs, scores, r0, r1, n):
     """Local (r1-r0, n) block with the stripe's scores (zeros elsewhere, as the memmap)."""
     import torch

@@ -10,6 +10,8 @@ Readers, in order:
   2. the same path with the suffix `.npz` (np.load, allow_pickle=False), nested keys
      flattened as 'madmom_features/onsets'. This image has neither h5py nor PyTables, so the
      tests and the synthetic datasets use this form (`save_features`).
+An HDF5 dataset compressed with a filter h5py cannot decode (deepdish's default blosc, without
+the plugin) raises IOError naming the filter and the one-line .npz conversion.
 """
 import os
 
@@ -45,6 +47,40 @@ def _flatten(feats, prefix=""):
     return flat
 
 
+# HDF5 filter codes h5py cannot decode without a plugin (deepdish writes through PyTables with
+# blosc by default)
+_FILTER_NAMES = {32001: "blosc", 32004: "lz4", 32008: "bitshuffle", 32015: "zstd", 307: "bzip2"}
+
+CONVERT_RECIPE = ("convert the file once on a machine with deepdish: `import deepdish as dd; "
+                  "from acoss.features_io import save_features; save_features(path, dd.io.load(path))` "
+                  "(writes the .npz twin this reader takes), or install the filter plugin (hdf5plugin)")
+
+
+def _missing_filters(h5py, ds):
+    """Names of the dataset's HDF5 filters that this h5py/libhdf5 cannot apply."""
+    out = []
+    plist = ds.id.get_create_plist()
+    for i in range(plist.get_nfilters()):
+        code, _, _, name = plist.get_filter(i)
+        if not h5py.h5z.filter_avail(code):
+            nm = name.decode(errors="replace") if isinstance(name, bytes) else str(name)
+            out.append("%s (filter %d)" % (_FILTER_NAMES.get(code, nm or "unknown"), code))
+    return out
+
+
+def _read_dataset(h5py, path, key, ds):
+    """ds[()], raising IOError that names the filter and the .npz conversion when the read fails
+    on a compression filter this libhdf5 lacks (h5py's own message names only a plugin dir)."""
+    try:
+        return ds[()]
+    except OSError as e:
+        missing = _missing_filters(h5py, ds)
+        if missing:
+            raise IOError("%s: dataset '%s' is compressed with %s, which this h5py cannot decode; %s"
+                          % (path, key, ", ".join(missing), CONVERT_RECIPE)) from e
+        raise
+
+
 def _load_h5(path):
     import h5py  # optional
 
@@ -54,7 +90,7 @@ def _load_h5(path):
             if isinstance(v, h5py.Group):
                 d[k] = walk(v)
             else:
-                a = v[()]
+                a = _read_dataset(h5py, path, v.name, v)
                 d[k] = a.decode() if isinstance(a, bytes) else a
         for k, v in g.attrs.items():
             if k not in d and not k.startswith("DEEPDISH") and not k.startswith("CLASS"):
@@ -77,13 +113,16 @@ def save_h5(path, mats, h5py):
 def load_features(path, keys=None):
     """Feature dict of one track; IOError if no readable file exists. keys: read only these
     top-level entries (e.g. the chroma type and 'label'); None reads the whole dict."""
+    p = _npz_path(path)
     if os.path.exists(path) and not path.endswith(".npz"):
         try:
             d = _load_h5(path)
             return d if keys is None else {k: d[k] for k in keys if k in d}
         except ImportError:
             pass
-    p = _npz_path(path)
+        except IOError:
+            if not os.path.exists(p):  # an undecodable filter and no converted twin
+                raise
     if os.path.exists(p):
         with np.load(p, allow_pickle=False) as z:
             names = z.files if keys is None else [k for k in z.files if k.split("/")[0] in keys]
@@ -104,8 +143,12 @@ def load_many(paths, keys=None, workers=None):
 
 
 def save_features(path, feats):
-    """Write `feats` as the .npz twin of `path` (creates the directory)."""
+    """Write `feats` as the .npz twin of `path` (creates the directory). Written to a temporary
+    name and renamed into place, so ranks caching the same song (EarlyFusion's block features)
+    never leave a torn file for each other."""
     p = _npz_path(path)
     os.makedirs(os.path.dirname(p) or ".", exist_ok=True)
-    np.savez(p, **_flatten(feats))
+    tmp = "%s.tmp%d.npz" % (p[:-4], os.getpid())
+    np.savez(tmp, **_flatten(feats))
+    os.replace(tmp, p)
     return p

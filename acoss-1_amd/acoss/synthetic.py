@@ -179,12 +179,15 @@ def pack(tracks):
     return feats, off, lens
 
 
-def write_feature_dataset(root, tracks, labels, with_mfcc=False, seed=SEED, beat_period=43):
+def write_feature_dataset(root, tracks, labels, with_mfcc=False, seed=SEED, beat_period=43, mfcc_shortfall=43):
     """Write a dataset the plugin classes can read: '<root>/dataset.csv' (work_id, track_id)
     and one feature file per track at '<root>/features/<work_id>/<track_id>.npz' with the keys
     of the reference's feature dicts (README.md:93-114): 'hpcp', 'crema', 'chroma_cens',
-    'label', 'track_id', and with_mfcc: 'mfcc_htk' (20, n) and 'madmom_features/onsets'
-    (a fixed beat grid with jitter). Returns (csv path, feature dir with trailing slash)."""
+    'label', 'track_id', and with_mfcc: 'mfcc_htk' (20, n - mfcc_shortfall) and
+    'madmom_features/onsets' (a fixed beat grid with jitter, up to the chroma's last frame). The
+    reference extractor's mfcc_htk has about 43 frames fewer than its hpcp (22050-sample windows
+    with validFrameThresholdRatio=1, acoss/features.py:884), so the last beats fall past the
+    MFCC's end as in real feature files. Returns (csv path, feature dir with trailing slash)."""
     from .features_io import save_features
     rng = np.random.Generator(np.random.PCG64(seed))
     feat_dir = os.path.join(root, "features") + "/"
@@ -195,7 +198,7 @@ def write_feature_dataset(root, tracks, labels, with_mfcc=False, seed=SEED, beat
         f = {"hpcp": t, "crema": t, "chroma_cens": t, "label": work, "track_id": track}
         if with_mfcc:
             n = len(t)
-            f["mfcc_htk"] = rng.standard_normal((20, n)).astype(np.float32)
+            f["mfcc_htk"] = rng.standard_normal((20, max(1, n - mfcc_shortfall))).astype(np.float32)
             beats = np.arange(0, n - 1, beat_period) + rng.integers(0, 3, size=len(range(0, n - 1, beat_period)))
             f["madmom_features"] = {"onsets": np.unique(np.clip(beats, 0, n - 1)).astype(np.int64)}
         save_features(feat_dir + work + "/" + track + ".h5", f)

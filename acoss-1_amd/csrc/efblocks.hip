@@ -100,6 +100,9 @@ __device__ void ef_resize(const float* X, int64_t ld, int n_in, int R, int D, do
 
 __global__ __launch_bounds__(256) void k_ef_blocks(const float* __restrict__ mfcc, const float* __restrict__ chroma,
                                                    const int64_t* __restrict__ frame_off,
+                                                   const int32_t* __restrict__ n_frames,
+                                                   const int64_t* __restrict__ mfcc_off,
+                                                   const int32_t* __restrict__ mfcc_frames,
                                                    const int64_t* __restrict__ onsets,
                                                    const int64_t* __restrict__ onset_off,
                                                    const int64_t* __restrict__ block_off, int n_tracks, int bs,
@@ -121,11 +124,14 @@ __global__ __launch_bounds__(256) void k_ef_blocks(const float* __restrict__ mfc
   const int tr = lo;
   const int b = (int)(gb - block_off[tr]);
   const int64_t* on = onsets + onset_off[tr];
-  const int64_t f0 = frame_off[tr];
-  // ---- MFCC block: resize, z-normalise
+  const int64_t f0 = frame_off[tr], m0 = mfcc_off[tr];
+  // ---- MFCC block: resize, z-normalise. The span is mfcc[o[b] : o[b + bs - 1]] clamped to the
+  // MFCC's own frame count, as Python slicing clamps (the extractor's mfcc_htk has fewer frames
+  // than the chroma, features.py:884); the host checked that every clamped span is non-empty.
   {
-    const int i1 = (int)on[b], i2 = (int)on[b + bs - 1];
-    ef_resize(mfcc + (f0 + i1) * Dm, Dm, i2 - i1, Rm, Dm, xs, w, &s_rad);
+    const int nm = mfcc_frames[tr];
+    const int i1 = (int)on[b], i2 = min((int)on[b + bs - 1], nm);
+    ef_resize(mfcc + (m0 + i1) * Dm, Dm, i2 - i1, Rm, Dm, xs, w, &s_rad);
     if (threadIdx.x < Dm) {  // column means (sequential over the rows)
       double s = 0.0;
       for (int k = 0; k < Rm; ++k) s += xs[k * Dm + threadIdx.x];
@@ -170,9 +176,9 @@ __global__ __launch_bounds__(256) void k_ef_blocks(const float* __restrict__ mfc
     }
     __syncthreads();
   }
-  // ---- chroma block: resize
+  // ---- chroma block: resize (span clamped to the chroma's frame count, likewise)
   {
-    const int i1 = (int)on[b], i2 = (int)on[b + bs];
+    const int i1 = (int)on[b], i2 = min((int)on[b + bs], (int)n_frames[tr]);
     ef_resize(chroma + (f0 + i1) * 12, 12, i2 - i1, Rc, 12, xs, w, &s_rad);
     float* oc = out_chroma + gb * (int64_t)(Rc * 12);
     for (int e = threadIdx.x; e < Rc * 12; e += blockDim.x) oc[e] = (float)xs[e];
@@ -234,7 +240,8 @@ __global__ __launch_bounds__(256) void k_track_median(const float* __restrict__ 
 using namespace acoss;
 
 extern "C" int acoss_ef_block_features(const float* mfcc, const float* chroma, const int64_t* frame_off,
-                                       const int32_t* n_frames, const int64_t* onsets, const int64_t* onset_off,
+                                       const int32_t* n_frames, const int64_t* mfcc_off,
+                                       const int32_t* mfcc_frames, const int64_t* onsets, const int64_t* onset_off,
                                        const int64_t* block_off, int32_t n_tracks, int64_t total_blocks,
                                        int32_t blocksize, int32_t mfccs_per_block, int32_t chromas_per_block,
                                        int32_t d_mfcc, float* out_mfcc, float* out_ssm, float* out_chroma,
@@ -246,15 +253,15 @@ extern "C" int acoss_ef_block_features(const float* mfcc, const float* chroma, c
     return ACOSS_E_ARG;
   }
   if (n_tracks == 0) return ACOSS_OK;
-  if (!chroma || !frame_off || !n_frames || !out_med || (total_blocks > 0 && (!mfcc || !onsets || !onset_off ||
+  if (!chroma || !frame_off || !n_frames || !out_med || (total_blocks > 0 && (!mfcc || !mfcc_off || !mfcc_frames || !onsets || !onset_off ||
       !block_off || !out_mfcc || !out_ssm || !out_chroma))) {
     set_error("acoss_ef_block_features: NULL pointer");
     return ACOSS_E_ARG;
   }
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   if (total_blocks > 0) {
-    hipLaunchKernelGGL(k_ef_blocks, dim3((unsigned)total_blocks), dim3(256), 0, s, mfcc, chroma, frame_off, onsets,
-                       onset_off, block_off, n_tracks, blocksize, mfccs_per_block, chromas_per_block, d_mfcc,
+    hipLaunchKernelGGL(k_ef_blocks, dim3((unsigned)total_blocks), dim3(256), 0, s, mfcc, chroma, frame_off, n_frames,
+                       mfcc_off, mfcc_frames, onsets, onset_off, block_off, n_tracks, blocksize, mfccs_per_block, chromas_per_block, d_mfcc,
                        out_mfcc, out_ssm, out_chroma);
     ACOSS_LAUNCH_CHECK();
   }

@@ -70,15 +70,39 @@ def log(msg):
 T_START = time.perf_counter()
 
 
+def cgroup_cpu_quota():
+    """CPUs the cgroup's CFS quota grants this process (cgroup v2 cpu.max or v1
+    cpu.cfs_quota_us / cpu.cfs_period_us), None when unlimited or unreadable, and the source."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            return (None if q == "max" else float(q) / float(per)), path
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return (None if q <= 0 else q / per), "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"
+    except (OSError, ValueError):
+        return None, None
+
+
 def cpu_share():
-    """Threads for the CPU baseline: the CPU share the GPU box grants one GPU (OMP_NUM_THREADS is
-    set to it there; nproc reports the whole machine), else the CPUs this process may run on."""
+    """(threads, how they were chosen) for the CPU baselines: every CPU the box grants this
+    process. A CFS quota, when there is one, bounds the affinity mask; without one the box's
+    per-GPU CPU share is what it exports as OMP_NUM_THREADS (nproc and the affinity mask there
+    show the whole machine); else every CPU in the affinity mask."""
     n = len(os.sched_getaffinity(0))
+    quota, _ = cgroup_cpu_quota()
+    if quota:
+        return max(1, min(n, int(math.floor(quota)))), "cgroup CFS quota"
     try:
         omp = int(os.environ.get("OMP_NUM_THREADS", "0"))
     except ValueError:
         omp = 0
-    return max(1, min(n, omp) if omp > 0 else n)
+    if 0 < omp < n:
+        return omp, "OMP_NUM_THREADS (the box's per-GPU CPU share; no CFS quota set)"
+    return n, "sched_getaffinity"
 
 
 ORACLE_FIXTURE = os.path.join(ROOT, "tests", "golden", "bench_oracle_qmax.npz")
@@ -197,11 +221,9 @@ def other_paths(nth, seed):
     ems = ev0.elapsed_time(ev1)
     flops = 2.0 * (1000 + 1225 + 480) * NB * NB
     esc = esc.cpu().numpy().reshape(-1, 4)
-    t0 = time.perf_counter()
-    agree = 0
-    ncpu = 24
-    for p in range(ncpu):
-        i, j = epairs[p * 97 % len(epairs)]
+
+    def ef_cpu_pair(p):
+        i, j = epairs[p]
         f1 = {"mfccs": mf[i * NB:(i + 1) * NB], "ssms": ss[i * NB:(i + 1) * NB], "chromas": ch[i * NB:(i + 1) * NB],
               "chroma_med": med[i]}
         f2 = {"mfccs": mf[j * NB:(j + 1) * NB], "ssms": ss[j * NB:(j + 1) * NB], "chromas": ch[j * NB:(j + 1) * NB],
@@ -213,7 +235,17 @@ def other_paths(nth, seed):
         for c in C:
             W += npo.getWCSM(c, 10, 10)
         ref = [oracle.sw_constrained(npo.csm_to_binary(M, 0.1)) for M in C + [np.exp(-W)]]
-        agree += int(np.sum(np.asarray(ref) == esc[p * 97 % len(epairs)]))
+        return int(np.sum(np.asarray(ref) == esc[p]))
+
+    # the same thread count as the Serra09 baseline: one pair per thread at a time, BLAS held to one
+    # thread per worker so the threads do not oversubscribe the cores
+    from concurrent.futures import ThreadPoolExecutor
+    from threadpoolctl import threadpool_limits
+    ncpu = 24 * nth
+    sample = [p * 97 % len(epairs) for p in range(ncpu)]
+    t0 = time.perf_counter()
+    with threadpool_limits(limits=1), ThreadPoolExecutor(max_workers=nth) as ex:
+        agree = sum(ex.map(ef_cpu_pair, sample))
     cdt = time.perf_counter() - t0
     res["earlyfusion"] = {"metric": "song-pairs/s (EarlyFusion: 3 CSMs + kNN + WCSM fusion + 4 SW, 446 blocks)",
                           "value": round(len(epairs) / (ems * 1e-3), 1), "ms": round(ems, 3),
@@ -223,29 +255,33 @@ def other_paths(nth, seed):
                                        "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
                                        "frac": round(flops * len(epairs) / (ems * 1e-3) / 1e12 / PEAK_F32_TFLOPS, 4),
                                        "flops_per_pair": flops},
-                          "cpu_baseline": {"value": round(ncpu / cdt, 3), "cores": 1, "kind": "port",
-                                           "sample": "%d pairs, numpy restatement + C SW oracle, %.1f s" % (ncpu, cdt)},
+                          "cpu_baseline": {"value": round(ncpu / cdt, 3), "cores": nth, "kind": "port",
+                                           "per_thread": round(ncpu / cdt / nth, 3),
+                                           "sample": "%d pairs, numpy restatement + C SW oracle on %d threads "
+                                                     "(BLAS 1 thread each), %.1f s" % (ncpu, nth, cdt)},
                           "scores_equal_to_oracle": "%d of %d" % (agree, 4 * ncpu)}
     # ---- SNF cross-diffusion step (f2) at Da-TACOS size
     res["snf"] = snf_path(seed)
     return res
 
 
-def snf_path(seed, n=15000, L=2, K=20, n_cpu=2000):
+def snf_path(seed, n=15000, L=2, K=20):
     """One SNF cross-diffusion step (acoss_snf_step, similarity_fusion.py:163-174) on n x n float64
     matrices, n = 15,000 (Da-TACOS), L = 2 (ChenFusion), K = 20; HBM-bound: algorithmic bytes
-    (L + 4) * 8 n^2 per step. The CPU sample is the reference's own scipy expression
-    (np_oracle.snf_step, one core) at n = n_cpu, with the GPU step at that size checked against it."""
+    (L + 4) * 8 n^2 per step. The CPU baseline is the reference's own scipy
+    expression (np_oracle.snf_step; scipy's sparse products are single-threaded, so one core) on
+    the SAME inputs at the same n, and the GPU step is checked against it bit for bit."""
     import torch
     from acoss import _lib
     from oracle import np_oracle as npo
-    g = torch.Generator(device="cuda").manual_seed(seed)
-    mats = [torch.rand((n, n), dtype=torch.float64, device="cuda", generator=g) for _ in range(L)]
-    W = torch.rand((n, n), dtype=torch.float32, device="cuda", generator=g)
-    V, J = torch.topk(W, K, dim=1)
-    del W
-    V = (V / V.sum(1, keepdim=True)).to(torch.float64)
-    J = J.to(torch.int32)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cm = [rng.random((n, n)) for _ in range(L)]
+    cJ = np.stack([rng.choice(n, K, replace=False) for _ in range(n)]).astype(np.int32)
+    cV = rng.random((n, K))
+    cV /= cV.sum(1, keepdims=True)
+    mats = [torch.as_tensor(m).cuda() for m in cm]
+    J = torch.as_tensor(cJ).cuda()
+    V = torch.as_tensor(cV).cuda()
     out = torch.empty((n, n), dtype=torch.float64, device="cuda")
     _lib.snf_step(mats, 0, J, V, 1.0, out=out)
     torch.cuda.synchronize()
@@ -254,31 +290,29 @@ def snf_path(seed, n=15000, L=2, K=20, n_cpu=2000):
     ts = []
     for r in range(5):
         ev0.record(s)
-        _lib.snf_step(mats, r % L, J, V, 1.0, out=out, validated=True)
+        _lib.snf_step(mats, 0, J, V, 1.0, out=out, validated=True)
         ev1.record(s)
         ev1.synchronize()
         ts.append(ev0.elapsed_time(ev1))
     ms = float(np.median(ts))
+    got = out.cpu().numpy()
     del mats, out
     torch.cuda.empty_cache()
     algo = (L + 4) * 8.0 * n * n
-    rng = np.random.Generator(np.random.PCG64(seed))
-    cm = [rng.random((n_cpu, n_cpu)) for _ in range(L)]
-    cJ = np.stack([rng.choice(n_cpu, K, replace=False) for _ in range(n_cpu)]).astype(np.int32)
-    cV = rng.random((n_cpu, K))
-    cV /= cV.sum(1, keepdims=True)
     t0 = time.perf_counter()
     ref = npo.snf_step(cm, 0, cJ, cV, 1.0)
     cdt = time.perf_counter() - t0
-    got = _lib.snf_step([torch.as_tensor(m).cuda() for m in cm], 0, cJ, cV, 1.0).cpu().numpy()
+    same = bool(np.array_equal(got, ref))
+    del ref, got, cm
     return {"metric": "SNF cross-diffusion steps/s (n = %d, L = %d, K = %d)" % (n, L, K),
             "value": round(1e3 / ms, 2), "ms": round(ms, 3), "dtype": "f64",
             "roofline": {"bound": "hbm", "achieved": round(algo / (ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": round(algo / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                          "bytes_per_step": algo},
-            "cpu_baseline": {"value": round(1.0 / cdt, 3), "cores": 1, "kind": "port",
-                             "sample": "one step at n = %d (scipy csr, np_oracle.snf_step), %.2f s" % (n_cpu, cdt)},
-            "bitexact_vs_scipy_n%d" % n_cpu: bool(np.array_equal(got, ref))}
+            "cpu_baseline": {"value": round(1.0 / cdt, 4), "cores": 1, "kind": "port",
+                             "sample": "one step at the same n = %d on the same inputs (scipy csr, "
+                                       "np_oracle.snf_step, single-threaded), %.1f s" % (n, cdt)},
+            "bitexact_vs_scipy": same}
 
 
 def host_info():
@@ -291,8 +325,10 @@ def host_info():
                     break
     except OSError:
         pass
+    quota, qsrc = cgroup_cpu_quota()
     return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model,
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cgroup_cpu_quota": quota,
+            "cgroup_quota_file": qsrc}
 
 
 def corpus_tracks(n_gpus, frames, seed, kind="hard"):
@@ -332,6 +368,56 @@ def corpus_tracks(n_gpus, frames, seed, kind="hard"):
     return tracks, np.asarray(labels, np.int32)
 
 
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, script=None, argv=None):
+    """`bench.py --gpus N` run without a launcher (no WORLD_SIZE in the environment): start N
+    rank processes of this same command line, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT set, as torch.distributed.run would. This parent never
+    touches the GPU. Rank 0's stdout (the JSON line) is relayed; every rank's stderr passes
+    through. If any rank fails the others are stopped and the exit status is non-zero."""
+    import subprocess
+    import tempfile
+    port = _free_port()
+    out0 = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ACOSS_BENCH_LAUNCHER="self")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        cmd = [sys.executable, script or os.path.abspath(__file__)] + list(sys.argv[1:] if argv is None else argv)
+        procs.append(subprocess.Popen(cmd, env=env,
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            log("a rank exited with status %d: stopping the others" % rc)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    out0.seek(0)
+    sys.stdout.write(out0.read())
+    sys.stdout.flush()
+    return rc if rc > 0 else (1 if rc else 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -348,19 +434,32 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-paths", action="store_true", help="skip the SiMPle / EarlyFusion lines")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args.gpus)  # before anything touches the GPU
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d: launch one rank per GPU with "
+                         "--nproc-per-node equal to --gpus (or run without a launcher and let bench.py start "
+                         "the ranks)" % (args.gpus, world))
 
     import torch
     import torch.distributed as dist
     from acoss import _lib, distributed, evaluation
     from acoss.engine import ChromaBank
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU over RCCL ("nccl"); ACOSS_DIST_BACKEND=gloo rehearses the multi-rank
     # path with several ranks sharing one GPU (the stripes are exchanged through host memory)
     backend = os.environ.get("ACOSS_DIST_BACKEND", "nccl")
-    dev = local % max(1, torch.cuda.device_count())
+    n_dev = torch.cuda.device_count()
+    if world > 1 and backend == "nccl" and n_dev < world:
+        raise SystemExit("bench.py: %d ranks over RCCL need %d GPUs, %d visible (ACOSS_DIST_BACKEND=gloo "
+                         "rehearses several ranks on one GPU)" % (world, world, n_dev))
+    dev = local % max(1, n_dev)
     torch.cuda.set_device(dev)
     if world > 1:
         if backend == "nccl":
@@ -496,11 +595,11 @@ def main():
         if world == 1 and args.corpus == "hard":
             map_parity = oracle_map_parity(tracks, labels, lens, my_pairs_np, Dfull, Dsym, args.frames,
                                            (MR, MRR, MDR, MAP, tops))
-        if args.cpu_sample != 0:
+        nth, nth_src = (args.cpu_threads, "--cpu-threads") if args.cpu_threads else cpu_share()
+        if args.cpu_sample != 0 and world == 1:  # the CPU baseline: rank 0 at N = 1 only
             import oracle
             from acoss.synthetic import pack
             feats, off, ln = pack(tracks)
-            nth = args.cpu_threads or cpu_share()
             rng = np.random.Generator(np.random.PCG64(1234))
             k = min(args.cpu_sample if args.cpu_sample > 0 else len(my_pairs_np), len(my_pairs_np))
             sp = my_pairs_np[np.sort(rng.choice(len(my_pairs_np), size=k, replace=False))]
@@ -512,16 +611,17 @@ def main():
             cdt = time.perf_counter() - t0
             gq = Dfull[sp[:, 0], sp[:, 1]]
             cpu = {"value": round(len(sp) / cdt, 3), "unit": "song-pairs/s", "cores": nth, "kind": "port",
-                   "sample": "%s (%dx%d frames), oracle/crp_oracle.cpp, %d OpenMP threads (the box's CPU share), "
-                             "%.1f s" % (what, args.frames, args.frames, nth, cdt),
+                   "per_thread": round(len(sp) / cdt / nth, 3), "threads_from": nth_src,
+                   "sample": "%s (%dx%d frames), oracle/crp_oracle.cpp, %d OpenMP threads (%s), "
+                             "%.1f s" % (what, args.frames, args.frames, nth, nth_src, cdt),
                    "host": host_info(),
                    "qmax_bitexact_vs_gpu": bool(np.array_equal(gq.astype(np.float32), q)),
                    "qmax_pairs_differing": int(np.sum(gq.astype(np.float32) != q))}
 
         paths = None
         if world == 1 and not args.no_paths:
-            log("other paths (SiMPle, EarlyFusion)")
-            paths = other_paths(args.cpu_threads or cpu_share(), args.seed)
+            log("other paths (SiMPle, EarlyFusion, SNF)")
+            paths = other_paths(nth, args.seed)
 
         result = {
             "metric": "song-pairs/sec (CSM+Qmax) on 12-d HPCP, ~2000 frames/track; MAP parity",
@@ -538,12 +638,40 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu,
             "speedup_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
             "other_paths": paths,
+            "launch": {"world": world, "device_count": n_dev, "backend": backend if world > 1 else None,
+                       "launcher": os.environ.get("ACOSS_BENCH_LAUNCHER", "external" if world > 1 else None)},
         }
+    if world > 1 and not args.no_paths:
+        # SNF late fusion at Da-TACOS size across the ranks: the measured sharding decision
+        # (similarity_fusion.shard_plan: one replicated step vs one all-gather of B, max over ranks)
+        log("SNF sharding plan (n = 15,000)")
+        snf = snf_shard_probe(world, rank, args.seed)
+        if result is not None:
+            result["snf_plan"] = snf
+    if result is not None:
         print(json.dumps(result))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
+
+
+def snf_shard_probe(world, rank, seed, n=15000, L=2, K=20):
+    """similarity_fusion.shard_plan on ChenFusion-shaped inputs (L = 2 float64 n x n matrices, K = 20)
+    at Da-TACOS size: times one replicated acoss_snf_step and one all-gather of B's row stripes
+    (RCCL over xGMI under the nccl backend), and reports the decision the fusion would take."""
+    import torch
+    from acoss.algorithms.utils import similarity_fusion as sf
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    Pts = [torch.rand((n, n), dtype=torch.float64, device="cuda", generator=g) for _ in range(L)]
+    rng = np.random.Generator(np.random.PCG64(seed))
+    J = torch.as_tensor(np.stack([rng.choice(n, K, replace=False) for _ in range(n)]).astype(np.int32)).cuda()
+    V = torch.as_tensor(rng.random((n, K))).cuda()
+    plan = sf.shard_plan(Pts, [J] * L, [V] * L, 1.0, world, rank, force=None)
+    del Pts
+    torch.cuda.empty_cache()
+    return plan
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

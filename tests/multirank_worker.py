@@ -36,6 +36,15 @@ def main():
             # SNF late fusion (latefusion_chen.py:87-91): row-sharded across the ranks
             a.normalize_by_length()
             a.do_late_fusion()
+    elif algo == "EarlyFusion":
+        # config 5's flow (coverid.py:72-88): block features, the four scores of the stripe on the
+        # device, one all-gather per score, then SNF late and early+late (row-sharded when
+        # ACOSS_SNF_SHARD=1)
+        from acoss.algorithms.earlyfusion_traile import EarlyFusion
+        a = EarlyFusion(csv, fdir, shortname="mr", cachedir=cachedir)
+        a.prepare()
+        a.all_pairwise(symmetric=True)
+        a.do_late_fusion()
     else:
         from acoss.algorithms.simple_silva import Simple
         a = Simple(csv, fdir, shortname="mr", cachedir=cachedir)

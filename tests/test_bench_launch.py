@@ -1,0 +1,60 @@
+"""bench.py's multi-rank launch contract (CPU): `--gpus N` must never silently measure fewer ranks.
+
+* WORLD_SIZE set by a launcher but different from --gpus: bench.py refuses, before touching torch.
+* --gpus N without a launcher: bench.py starts N rank processes itself (launch_ranks); when a rank
+  fails (here: no GPU in this container) the parent stops the others and exits non-zero.
+"""
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env_extra, timeout=240):
+    env = dict(os.environ, **env_extra)
+    for k in ("RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    if "WORLD_SIZE" not in env_extra:
+        env.pop("WORLD_SIZE", None)
+    return subprocess.run([sys.executable, BENCH] + args, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def test_world_size_mismatch_fails_loudly():
+    r = _run(["--gpus", "8", "--steps", "1", "--warmup", "0"], {"WORLD_SIZE": "1"})
+    assert r.returncode != 0
+    assert "--gpus 8 but WORLD_SIZE=1" in r.stderr
+    assert r.stdout.strip() == ""  # no JSON line for a run that did not happen
+
+
+def test_self_launch_propagates_rank_failure():
+    # two ranks, no GPU here: every rank fails at its first GPU call; the parent must report it
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-paths", "--cpu-sample", "0"],
+             {"ACOSS_DIST_BACKEND": "gloo"})
+    assert r.returncode != 0, r.stderr[-2000:]
+    assert r.stdout.strip() == ""
+
+
+def test_launch_ranks_env(tmp_path, monkeypatch):
+    """launch_ranks gives rank r the torch.distributed.run environment (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR 127.0.0.1, one MASTER_PORT) and relays only rank 0's stdout."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    script = tmp_path / "rank.py"
+    script.write_text("import os, json\nprint(json.dumps({k: os.environ[k] for k in ('RANK', 'LOCAL_RANK', "
+                      "'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT', 'ACOSS_BENCH_LAUNCHER')}))\n")
+    import io
+    buf = io.StringIO()
+    monkeypatch.setattr(sys, "stdout", buf)
+    assert bench.launch_ranks(3, script=str(script), argv=[]) == 0
+    import json
+    lines = [ln for ln in buf.getvalue().splitlines() if ln.strip()]
+    assert len(lines) == 1
+    env0 = json.loads(lines[0])
+    assert env0["RANK"] == "0" and env0["LOCAL_RANK"] == "0" and env0["WORLD_SIZE"] == "3"
+    assert env0["MASTER_ADDR"] == "127.0.0.1" and int(env0["MASTER_PORT"]) > 0
+    assert env0["ACOSS_BENCH_LAUNCHER"] == "self"

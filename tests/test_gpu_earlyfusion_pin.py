@@ -161,13 +161,23 @@ def test_ef_block_features_gpu_vs_restatement():
     rng = np.random.default_rng(12)
     chromas, mfccs, onsets = [], [], []
     # (16000, 700): beat blocks of ~14,000 frames, Gaussian radii past the LDS tap table (on-the-fly taps)
-    for n, period in [(900, 43), (2601, 37), (500, 11), (4001, 60), (860, 43), (16000, 700)]:
+    # (n, period, MFCC frames short of the chroma): the extractor's mfcc_htk is ~43 frames shorter
+    # (acoss/features.py:884), so the last beat blocks' MFCC spans are clamped by the slicing
+    # (resize_block's X[i1:i2]); (1200, 5, 100) cuts the last 20 blocks' MFCC spans short, the
+    # last one to 5 frames; "dup" repeats onsets (np.round of close beats), which the reference
+    # accepts while every block spans frames
+    for n, period, short in [(900, 43, 0), (2601, 37, 43), (500, 11, 43), (4001, 60, 0), (860, 43, 43),
+                             (16000, 700, 43), (1200, 5, 100)]:
         chromas.append(np.abs(rng.normal(size=(n, 12))).astype(np.float32))
-        m = rng.normal(size=(20, n)).astype(np.float32)
+        m = rng.normal(size=(20, n - short)).astype(np.float32)
         m[1, 5] = np.nan
         mfccs.append(m)
         o = np.arange(0, n - 1, period) + rng.integers(0, 4, size=len(range(0, n - 1, period)))
         onsets.append(np.unique(np.clip(o, 0, n - 1)).astype(np.int64))
+    dup = onsets[2].copy()
+    dup[10:14] = dup[10]  # four equal onsets inside a 20-beat block
+    onsets[2] = np.sort(dup)
+    assert onsets[6][-21] < mfccs[6].shape[1] < onsets[6][-2]  # the last blocks' spans end past the MFCC
     out = _lib.ef_block_features(chromas, [m.T for m in mfccs], onsets)
     tot, same = 0, 0
     for t in range(len(chromas)):
@@ -188,6 +198,14 @@ def test_ef_block_features_gpu_vs_restatement():
         npo.ef_block_features(short[0], rng.normal(size=(20, 300)).astype(np.float32), np.arange(1, 300, 90))
     with pytest.raises(ValueError):
         _lib.ef_block_features(short, [rng.normal(size=(300, 20)).astype(np.float32)], [np.arange(1, 300, 90)])
+    # a block whose MFCC span is empty after the clamp: the reference's resize raises, so does this
+    ch = np.abs(rng.normal(size=(400, 12))).astype(np.float32)
+    o = np.arange(0, 400, 10).astype(np.int64)
+    mf = rng.normal(size=(20, 150)).astype(np.float32)  # o[20] = 200 > 150 frames of MFCC
+    with pytest.raises(Exception):
+        npo.ef_block_features(ch, mf, o)
+    with pytest.raises(ValueError):
+        _lib.ef_block_features([ch], [mf.T], [o])
 
 
 _EF_KERNEL_SCRIPT = r"""

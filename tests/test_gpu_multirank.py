@@ -1,8 +1,9 @@
 """The real HIP scorers under torch.distributed: 2 gloo ranks sharing one GPU each score a
 row stripe of a Da-TACOS-shaped mini corpus (13-song cliques plus singletons, ragged
-lengths) through Serra09 / ChenFusion / Simple.all_pairwise (algorithm_template.py:142-193),
-all-gather, symmetrise on the device; the assembled Ds must equal the world-1 run bit for bit.
-ChenFusion's SNF late fusion runs row-sharded across the same two ranks.
+lengths) through Serra09 / ChenFusion / Simple / EarlyFusion.all_pairwise
+(algorithm_template.py:142-193), all-gather, symmetrise on the device; the assembled Ds must
+equal the world-1 run bit for bit. ChenFusion's and EarlyFusion's SNF late fusions run
+row-sharded (and, for EarlyFusion, replicated) across the same two ranks.
 Ranks are child processes (subprocess), one GPU context each (3 with the parent)."""
 import os
 import socket
@@ -38,18 +39,18 @@ def datacos_mini(tmp_path_factory):
             seq = base if v == 0 else synthetic.cover_of(rng, base)
             tracks.append(synthetic.render(rng, seq))
             labels.append(lab)
-    csv, fdir = synthetic.write_feature_dataset(str(root), tracks, np.asarray(labels))
+    csv, fdir = synthetic.write_feature_dataset(str(root), tracks, np.asarray(labels), with_mfcc=True)
     return root, csv, fdir
 
 
-def _run(algo, world, root, csv, fdir, tag):
+def _run(algo, world, root, csv, fdir, tag, env_extra=None):
     out = str(root / ("%s_%s_w%d.npz" % (algo, tag, world)))
     cache = str(root / ("cache_%s_%s_w%d" % (algo, tag, world)))
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0", **(env_extra or {}))
         procs.append(subprocess.Popen([sys.executable, WORKER, algo, csv, fdir, cache, out], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
@@ -85,8 +86,24 @@ def test_late_fusion_sharded_equals_world1(datacos_mini):
     single-process fusion bit for bit."""
     root, csv, fdir = datacos_mini
     d1 = _run("ChenLate", 1, root, csv, fdir, "a")
-    d2 = _run("ChenLate", 2, root, csv, fdir, "b")
+    d2 = _run("ChenLate", 2, root, csv, fdir, "b", {"ACOSS_SNF_SHARD": "1"})
     assert set(d1) == set(d2) and "Late" in d1
     assert np.count_nonzero(d1["Late"]) > 48 * 30
     for k in d1:
         np.testing.assert_array_equal(d2[k], d1[k])
+
+
+@pytest.mark.parametrize("shard", ["1", "0"])
+def test_earlyfusion_world2_equals_world1(datacos_mini, shard):
+    """EarlyFusion (config 5) across two ranks: each scores its block-count-balanced stripe with
+    the batched HIP scorer (_device_scores), the four score matrices are all-gathered, and the
+    SNF late / early+late fusions run row-sharded (shard=1) or replicated on every rank (0): all
+    six matrices equal the world-1 run bit for bit."""
+    root, csv, fdir = datacos_mini
+    d1 = _run("EarlyFusion", 1, root, csv, fdir, "a")
+    d2 = _run("EarlyFusion", 2, root, csv, fdir, "b" + shard, {"ACOSS_SNF_SHARD": shard})
+    assert set(d1) == set(d2) == {"mfccs", "ssms", "chromas", "early", "late", "early+late"}
+    for k in d1:
+        assert d1[k].shape == (48, 48)
+        assert np.count_nonzero(d1[k]) > 48 * 30, k
+        np.testing.assert_array_equal(d2[k], d1[k], err_msg=k)

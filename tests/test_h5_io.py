@@ -49,6 +49,25 @@ with h5py.File(path, "w") as f:
 d = features_io.load_features(path)
 assert np.array_equal(d["hpcp"], hpcp) and d["label"] == "W1" and d["track_id"] == "T1"
 assert np.array_equal(d["madmom_features"]["onsets"], np.arange(0, 50, 7))
+# a blosc-compressed dataset (deepdish's default through PyTables) without the filter plugin:
+# the chunk is stored as if blosc had been applied, so libhdf5 cannot read it; the reader must
+# raise IOError naming blosc and the .npz conversion, not h5py's plugin-directory message
+if not h5py.h5z.filter_avail(32001):
+    bpath = os.path.join(tmp, "W1", "T2.h5")
+    with h5py.File(bpath, "w") as f:
+        ds = f.create_dataset("hpcp", shape=(50, 12), dtype="f4", chunks=(50, 12), compression=32001,
+                              allow_unknown_filter=True)
+        ds.id.write_direct_chunk((0, 0), hpcp.tobytes()[:1000], filter_mask=0)
+        f.attrs["label"] = "W1"
+    try:
+        features_io.load_features(bpath)
+        raise SystemExit("no error on a blosc dataset")
+    except IOError as e:
+        msg = str(e)
+        assert "blosc" in msg and "save_features" in msg and "hpcp" in msg, msg
+    # once converted (the .npz twin beside it), the same path reads
+    features_io.save_features(bpath, {"hpcp": hpcp, "label": "W1"})
+    assert np.array_equal(features_io.load_features(bpath)["hpcp"], hpcp)
 print("OK")
 '''
 

@@ -65,32 +65,55 @@ def _inputs(n, L, seed):
     return Ws
 
 
-def _rank_worker(rank, world, port, n, L, K, niters, out):
+def _rank_worker(rank, world, port, n, L, K, niters, out, mode):
+    import json
+    import os
     import torch
     import torch.distributed as dist
+    os.environ["ACOSS_SNF_SHARD"] = mode
     _fake_lib(setattr)
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     from acoss.algorithms.utils import similarity_fusion as sf
     F = sf._fusion_ws([torch.as_tensor(W) for W in _inputs(n, L, 3)], K, niters, 1)
     np.save(out % rank, F.numpy())
+    with open((out % rank) + ".plan.json", "w") as f:
+        json.dump(sf.LAST_PLAN, f)
     dist.barrier()
     dist.destroy_process_group()
 
 
+def _world(tmp_path, world, n, L, K, niters, mode):
+    import json
+    import torch.multiprocessing as mp
+    out = str(tmp_path / ("%s_rank%%d.npy" % mode))
+    mp.start_processes(_rank_worker, args=(world, _free_port(), n, L, K, niters, out, mode), nprocs=world,
+                       join=True, start_method="spawn")
+    res = [np.load(out % r) for r in range(world)]
+    plans = [json.load(open((out % r) + ".plan.json")) for r in range(world)]
+    return res, plans
+
+
 @pytest.mark.parametrize("world,n,L", [(2, 37, 2), (3, 50, 3)])
 def test_sharded_fusion_equals_world1(tmp_path, monkeypatch, world, n, L):
+    """Forced sharding (ACOSS_SNF_SHARD=1), forced replication (=0) and the measured rule (auto)
+    all give the world-1 result bit for bit; under auto every rank takes the same decision, from
+    the same max-over-ranks timings."""
     import torch
-    import torch.multiprocessing as mp
     from acoss.algorithms.utils import similarity_fusion as sf
     _fake_lib(monkeypatch.setattr)
     K, niters = 5, 4
     ref = sf._fusion_ws([torch.as_tensor(W) for W in _inputs(n, L, 3)], K, niters, 1).numpy()
     assert np.isfinite(ref).all() and ref.shape == (n, n)
-    out = str(tmp_path / "rank%d.npy")
-    mp.start_processes(_rank_worker, args=(world, _free_port(), n, L, K, niters, out), nprocs=world, join=True,
-                       start_method="spawn")
-    for r in range(world):
-        np.testing.assert_array_equal(np.load(out % r), ref)
+    for mode in ("1", "0", "auto"):
+        res, plans = _world(tmp_path, world, n, L, K, niters, mode)
+        for r in range(world):
+            np.testing.assert_array_equal(res[r], ref)
+        if mode == "0":
+            assert plans == [{}] * world  # replicated: no plan measured
+        else:
+            assert all(p == plans[0] for p in plans), plans  # one decision, identical on every rank
+            assert plans[0]["shard"] is (True if mode == "1" else plans[0]["rule_shard"])
+            assert plans[0]["n"] == n and plans[0]["world"] == world
 
 
 def test_shard_rows_cover():
