@@ -10,7 +10,8 @@ Ties: the reference's np.argsort(-D, 1) is unstable (:235), so its order among e
 is platform-dependent. Here ties are broken by the reference's own row reordering (cliques
 contiguous, larger cliques first, :220-230) made deterministic (stable sorts, members in
 ascending index). With tie-free scores the result equals the reference's exactly
-(tests/test_evaluation.py pins it against golden vectors captured from the reference).
+(tests/test_host.py::test_eval_statistics_golden pins it against golden vectors captured from
+the reference).
 """
 import os
 

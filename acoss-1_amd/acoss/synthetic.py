@@ -179,11 +179,12 @@ def pack(tracks):
     return feats, off, lens
 
 
-def write_feature_dataset(root, tracks, labels, with_mfcc=False, seed=SEED, beat_period=43, mfcc_shortfall=43):
+def write_feature_dataset(root, tracks, labels, with_mfcc=False, seed=SEED, beat_period=43, mfcc_shortfall=43,
+                          chroma_keys=("hpcp", "crema", "chroma_cens")):
     """Write a dataset the plugin classes can read: '<root>/dataset.csv' (work_id, track_id)
     and one feature file per track at '<root>/features/<work_id>/<track_id>.npz' with the keys
-    of the reference's feature dicts (README.md:93-114): 'hpcp', 'crema', 'chroma_cens',
-    'label', 'track_id', and with_mfcc: 'mfcc_htk' (20, n - mfcc_shortfall) and
+    of the reference's feature dicts (README.md:93-114): the chroma_keys ('hpcp', 'crema',
+    'chroma_cens', each the same array), 'label', 'track_id', and with_mfcc: 'mfcc_htk' (20, n - mfcc_shortfall) and
     'madmom_features/onsets' (a fixed beat grid with jitter, up to the chroma's last frame). The
     reference extractor's mfcc_htk has about 43 frames fewer than its hpcp (22050-sample windows
     with validFrameThresholdRatio=1, acoss/features.py:884), so the last beats fall past the
@@ -195,7 +196,7 @@ def write_feature_dataset(root, tracks, labels, with_mfcc=False, seed=SEED, beat
     for k, (t, lab) in enumerate(zip(tracks, labels)):
         work, track = "W%05d" % int(lab), "T%06d" % k
         t = np.asarray(t, np.float32)
-        f = {"hpcp": t, "crema": t, "chroma_cens": t, "label": work, "track_id": track}
+        f = dict({k: t for k in chroma_keys}, label=work, track_id=track)
         if with_mfcc:
             n = len(t)
             f["mfcc_htk"] = rng.standard_normal((20, max(1, n - mfcc_shortfall))).astype(np.float32)

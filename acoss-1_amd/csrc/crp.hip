@@ -1249,19 +1249,15 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
       const size_t per = align_up(ring_elems * 2, 256) + ctl_bytes;
       char* rw = static_cast<char*>(workspace(14, per * nbuf));
       if (!rw) return ACOSS_E_HIP;
-      // the counters must start at zero, and again whenever the buffer or the slot count changes
-      static void* ctl_ptr[3] = {nullptr, nullptr, nullptr};
-      static int ctl_slots[3] = {0, 0, 0};
+      // the ticket / generation counters start at zero on EVERY call that uses the ring (a few KB,
+      // stream-ordered before the sub-batches, whose side streams wait on an event recorded on s
+      // after it): no state carried between calls, devices or an aborted launch
       for (int b = 0; b < nbuf; ++b) {
         char* base = rw + per * b;
         char* ctl = base + align_up(ring_elems * 2, 256);
         rings[b] = HrRing{reinterpret_cast<uint16_t*>(base), reinterpret_cast<unsigned long long*>(ctl),
                           reinterpret_cast<unsigned*>(ctl + 8 * 16 * 8), S};
-        if (ctl_ptr[b] != ctl || ctl_slots[b] != S) {
-          ACOSS_HIP_CHECK(hipMemsetAsync(ctl, 0, ctl_bytes, s));
-          ctl_ptr[b] = ctl;
-          ctl_slots[b] = S;
-        }
+        ACOSS_HIP_CHECK(hipMemsetAsync(ctl, 0, ctl_bytes, s));
       }
     }
   }

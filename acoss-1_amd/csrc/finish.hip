@@ -25,7 +25,9 @@ namespace {
 
 constexpr int kTile = 64;
 
-__global__ __launch_bounds__(256) void k_ds_finish(const float* __restrict__ D, int32_t n, int64_t ld,
+// D and out may be the same matrix (every caller finishes in place), so neither is __restrict__:
+// each block loads both of its tiles into LDS before its barrier and stores after it.
+__global__ __launch_bounds__(256) void k_ds_finish(const float* D, int32_t n, int64_t ld,
                                                    const double* __restrict__ norm, int32_t symmetric, int32_t mode,
                                                    float* out) {
   __shared__ float A[kTile][kTile + 1];

@@ -17,7 +17,8 @@
 //   (Serra et al. 2009 NJP 11:093017, Serra/Gomez/Herrera 2008 OTI, Chen et al. 2017,
 //   essentia 2.1-beta6 docs) is restated below. PARITY WITH ESSENTIA IS UNPINNED: the
 //   reference's own tests hold no vector for it (test/basetest.py is an import smoke test);
-//   the conventions chosen are frozen by tests/test_oracle_kat.py.
+//   the conventions chosen are frozen by the known-answer tests test_kat_* in
+//   tests/test_oracle_golden.py.
 // * acoss smith_waterman_constrained (alignment_tools.py:7-46), bit-exact float64.
 // * acoss Simple.simple_sim (simple_silva.py:68-118), float64 (direct sums instead of the
 //   reference's FFT + STOMP updates; agrees to ~1e-12, pinned by tests/golden).

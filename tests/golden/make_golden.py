@@ -25,7 +25,8 @@ Captured (reference file:line):
 
 essentia's ChromaCrossSimilarity / CoverSongSimilarity (the Serra09/Chen CRP + Qmax/dmax)
 are NOT importable anywhere (no essentia): those rows are pinned by hand-derived
-known-answer tests in tests/test_oracle_kat.py instead ("parity unpinned" vs essentia).
+known-answer tests (test_kat_* in tests/test_oracle_golden.py) instead ("parity unpinned" vs
+essentia).
 """
 import importlib.util
 import os

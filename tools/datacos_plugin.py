@@ -1,0 +1,199 @@
+"""Configs 3 and 4 at full size through the reference's plugin API on ONE GPU (BASELINE.json
+configs[2..3]; VERDICT r03 "next" #3).
+
+    python tools/datacos_plugin.py --algo serra09|simple [--tracks 15000] [--frames 500]
+                                   [--sample 5000] [--out result.json]
+
+Builds the Da-TACOS benchmark clique structure (acoss/data/da-tacos_benchmark_subset.csv shape:
+1000 cliques x 13 + 2000 singletons = 15,000 songs) as per-song feature files in the reference's
+layout (<dir>/<work_id>/<track_id>, README.md:93-114), already at the pair kernel's length
+(500 +-10 % frames: a 4-minute track's HPCP after the x40 downsample), and runs the reference flow
+(coverid.py:57-70,124-139) on them:
+
+  serra09: Serra09(csv, dir, downsample_fac=1) -> all_pairwise(symmetric=True) (112.5 M unordered
+           pairs) -> normalize_by_length -> getEvalStatistics('main')
+  simple:  Simple(csv, dir, chroma_type='crema', WIN=2, SKIP=1) -> all_pairwise(symmetric=False)
+           (225.0 M ordered pairs) -> getEvalStatistics('main')
+
+and checks full-size properties of the result:
+  * Serra09: the raw Ds (before normalisation) is symmetric with a zero diagonal, finite everywhere;
+    SiMPle: finite off the diagonal;
+  * a seeded sample of --sample pairs equals the CPU oracle (oracle/, test infrastructure) exactly,
+    from the same inputs (Serra09: the feature files' chroma, since downsample_fac=1 is the
+    identity; SiMPle: the GPU's SiMPle features, themselves checked against the numpy restatement
+    on a few songs);
+  * MAP / MR1 / MRR / MDR / Top-k of the device evaluation (acoss_eval_ranks) equal the host
+    restatement of getEvalStatistics on the same matrix.
+Prints progress, per-stage wall times, peak host RSS, and one JSON line (also written to --out).
+"""
+import argparse
+import json
+import os
+import resource
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "acoss-1_amd")]
+
+import numpy as np  # noqa: E402
+
+
+def log(msg, t0=[time.perf_counter()]):
+    print("[datacos %.1fs] %s" % (time.perf_counter() - t0[0], msg), file=sys.stderr, flush=True)
+
+
+def rss_gb():
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6  # KB -> GB
+
+
+def corpus(n_tracks, frames, seed):
+    from acoss import synthetic
+    rng = np.random.Generator(np.random.PCG64(seed))
+    tracks, labels = [], []
+    for lab, size in enumerate(synthetic.clique_sizes("datacos")):
+        n0 = int(round(frames * rng.uniform(0.9, 1.1)))
+        base = synthetic.base_sequence(rng, n0)
+        for v in range(size):
+            seq = base if v == 0 else synthetic.cover_of(rng, base, int(round(n0 * rng.uniform(0.9, 1.1))))
+            tracks.append(synthetic.render(rng, seq))
+            labels.append(lab)
+        if len(tracks) >= n_tracks:
+            break
+    return tracks[:n_tracks], np.asarray(labels[:n_tracks], np.int32)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--algo", choices=["serra09", "simple"], default="serra09")
+    ap.add_argument("--tracks", type=int, default=15000)
+    ap.add_argument("--frames", type=int, default=500)
+    ap.add_argument("--sample", type=int, default=5000)
+    ap.add_argument("--seed", type=int, default=20250101)
+    ap.add_argument("--threads", type=int, default=16, help="CPU oracle threads for the sample")
+    ap.add_argument("--workdir", default=None)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import torch
+    import oracle
+    from acoss import evaluation, synthetic
+    from oracle import np_oracle as npo
+
+    stages = {}
+    t = time.perf_counter()
+    tracks, labels = corpus(a.tracks, a.frames, a.seed)
+    T = len(tracks)
+    lens = np.array([len(x) for x in tracks], np.int32)
+    work = a.workdir or tempfile.mkdtemp(prefix="datacos_")
+    key = "hpcp" if a.algo == "serra09" else "crema"
+    csv, fdir = synthetic.write_feature_dataset(work, tracks, labels, chroma_keys=(key,))
+    stages["write_features_s"] = round(time.perf_counter() - t, 2)
+    log("%d songs (%d cliques), frames %d..%d, feature files written in %.1f s" %
+        (T, len(set(labels.tolist())), lens.min(), lens.max(), stages["write_features_s"]))
+    cache = os.path.join(work, "cache")
+    torch.cuda.set_device(0)
+
+    t = time.perf_counter()
+    if a.algo == "serra09":
+        from acoss.algorithms.rqa_serra09 import Serra09
+        algo = Serra09(csv, fdir, chroma_type=key, shortname="datacos", downsample_fac=1, cachedir=cache)
+        symmetric = True
+    else:
+        from acoss.algorithms.simple_silva import Simple
+        algo = Simple(csv, fdir, chroma_type=key, shortname="datacos", WIN=2, SKIP=1, cachedir=cache)
+        symmetric = False
+    algo.prepare()
+    torch.cuda.synchronize()
+    stages["prepare_s"] = round(time.perf_counter() - t, 2)
+    log("prepare %.1f s" % stages["prepare_s"])
+
+    t = time.perf_counter()
+    algo.all_pairwise(symmetric=symmetric)
+    torch.cuda.synchronize()
+    stages["all_pairwise_s"] = round(time.perf_counter() - t, 2)
+    n_pairs = T * (T - 1) // (2 if symmetric else 1)
+    log("all_pairwise: %d pairs in %.1f s = %.0f pairs/s" % (n_pairs, stages["all_pairwise_s"],
+                                                             n_pairs / stages["all_pairwise_s"]))
+
+    checks = {}
+    D = np.asarray(algo.Ds["main"])
+    off = ~np.eye(T, dtype=bool)
+    checks["finite_off_diagonal"] = bool(np.isfinite(D[off]).all())
+    if symmetric:
+        checks["symmetric"] = bool(np.array_equal(D, D.T))
+        checks["diagonal_zero"] = bool(np.all(np.diag(D) == 0))
+    rng = np.random.Generator(np.random.PCG64(a.seed + 1))
+    if symmetric:
+        i = rng.integers(0, T, size=4 * a.sample)
+        j = rng.integers(0, T, size=4 * a.sample)
+        m = i < j
+        sp = np.unique(np.stack([i[m], j[m]], 1), axis=0)[:a.sample].astype(np.int32)
+    else:
+        i = rng.integers(0, T, size=2 * a.sample)
+        j = rng.integers(0, T, size=2 * a.sample)
+        m = i != j
+        sp = np.unique(np.stack([i[m], j[m]], 1), axis=0)[:a.sample].astype(np.int32)
+    t = time.perf_counter()
+    if a.algo == "serra09":
+        feats, foff, flen = synthetic.pack(tracks)
+        q, _, _ = oracle.crp_batch(feats, foff, flen, sp, dmax=False, nthreads=a.threads)
+        got = D[sp[:, 0], sp[:, 1]]
+        checks["feature_identity"] = bool(all(np.array_equal(algo.all_feats[k], tracks[k]) for k in range(0, T, 997)))
+    else:
+        feats = [algo.all_feats[k] for k in range(T)]
+        for k in range(0, T, 1499):
+            np.testing.assert_allclose(feats[k], npo.simple_features(tracks[k], win=2, skip=1), rtol=1e-12,
+                                       atol=1e-15)
+        checks["simple_features_vs_restatement_1e-12"] = True
+        flat = np.concatenate([f.ravel() for f in feats])
+        soff = np.concatenate([[0], np.cumsum([f.size for f in feats])[:-1]]).astype(np.int64)
+        slen = np.array([f.shape[1] for f in feats], np.int32)
+        cs, _ = oracle.simple_batch(flat, soff, slen, sp, nthreads=a.threads)
+        q = (-cs).astype(np.float32)
+        got = D[sp[:, 0], sp[:, 1]]
+    checks["sample_pairs"] = int(len(sp))
+    checks["sample_pairs_differing_from_oracle"] = int(np.sum(got != q))
+    stages["oracle_sample_s"] = round(time.perf_counter() - t, 2)
+    log("oracle sample: %d pairs, %d differ (%.1f s)" % (len(sp), checks["sample_pairs_differing_from_oracle"],
+                                                         stages["oracle_sample_s"]))
+    del D
+
+    if a.algo == "serra09":
+        t = time.perf_counter()
+        algo.normalize_by_length()
+        stages["normalize_s"] = round(time.perf_counter() - t, 2)
+    t = time.perf_counter()
+    MR, MRR, MDR, MAP, tops = algo.getEvalStatistics("main")
+    stages["eval_device_s"] = round(time.perf_counter() - t, 2)
+    t = time.perf_counter()
+    cliques = [sorted(algo.cliques[s]) for s in algo.cliques]
+    hMR, hMRR, hMDR, hMAP, htops = evaluation.eval_statistics_cliques(np.array(algo.Ds["main"], np.float32), cliques,
+                                                                     [1, 10, 100, 1000])
+    stages["eval_host_s"] = round(time.perf_counter() - t, 2)
+    checks["eval_device_equals_host"] = bool(MR == hMR and MRR == hMRR and MDR == hMDR and MAP == hMAP
+                                             and list(tops) == list(htops))
+    ok = all(v for k, v in checks.items() if isinstance(v, bool)) and checks["sample_pairs_differing_from_oracle"] == 0
+    res = {"algo": a.algo, "config": "Da-TACOS benchmark shape, %d songs (1000 x 13 + singletons), %d +-10 %% frames"
+                                     % (T, a.frames),
+           "api": ("Serra09(downsample_fac=1).all_pairwise(symmetric=True) -> normalize_by_length -> getEvalStatistics"
+                   if a.algo == "serra09" else
+                   "Simple(chroma_type='crema', WIN=2, SKIP=1).all_pairwise(symmetric=False) -> getEvalStatistics"),
+           "pairs": n_pairs, "pairs_per_s_all_pairwise": round(n_pairs / stages["all_pairwise_s"], 1),
+           "stages": stages, "peak_host_rss_gb": round(rss_gb(), 2),
+           "MAP": float(MAP), "MR1": float(MR), "MRR": float(MRR), "MDR": float(MDR), "top": [int(x) for x in tops],
+           "checks": checks, "ok": bool(ok), "gpu": torch.cuda.get_device_name(0)}
+    algo.cleanup_memmap()
+    if not a.workdir:
+        shutil.rmtree(work, ignore_errors=True)
+    line = json.dumps(res)
+    print(line, flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(line + "\n")
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
