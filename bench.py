@@ -413,7 +413,13 @@ def launch_ranks(n, script=None, argv=None):
             break
         time.sleep(0.2)
     out0.seek(0)
-    sys.stdout.write(out0.read())
+    # rank 0's JSON line only: the process group's own chatter (gloo prints its connection
+    # message to stdout) goes to stderr
+    for line in out0.read().splitlines():
+        if line.startswith("{") and line.rstrip().endswith("}"):
+            sys.stdout.write(line + "\n")
+        elif line.strip():
+            sys.stderr.write(line + "\n")
     sys.stdout.flush()
     return rc if rc > 0 else (1 if rc else 0)
 

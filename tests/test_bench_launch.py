@@ -39,13 +39,15 @@ def test_self_launch_propagates_rank_failure():
 
 def test_launch_ranks_env(tmp_path, monkeypatch):
     """launch_ranks gives rank r the torch.distributed.run environment (RANK, LOCAL_RANK,
-    WORLD_SIZE, MASTER_ADDR 127.0.0.1, one MASTER_PORT) and relays only rank 0's stdout."""
+    WORLD_SIZE, MASTER_ADDR 127.0.0.1, one MASTER_PORT) and relays only rank 0's JSON line (the
+    process group's own stdout chatter goes to stderr)."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
     script = tmp_path / "rank.py"
-    script.write_text("import os, json\nprint(json.dumps({k: os.environ[k] for k in ('RANK', 'LOCAL_RANK', "
+    script.write_text("import os, json\nprint('[Gloo] Rank 0 is connected to 2 peer ranks.')\n"
+                      "print(json.dumps({k: os.environ[k] for k in ('RANK', 'LOCAL_RANK', "
                       "'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT', 'ACOSS_BENCH_LAUNCHER')}))\n")
     import io
     buf = io.StringIO()
