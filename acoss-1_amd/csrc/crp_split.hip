@@ -25,6 +25,13 @@
 
 #include "crp_internal.hpp"
 
+#ifndef ACOSS_LW_SELECT  // (ACOSS_LW_SELECT: the round-3 compare/select placement, for A/B)
+// v_writelane_b32 through the LLVM intrinsic (hipcc has no builtin for it), so the compiler's
+// hazard recognizer inserts the wait state between the ballot's SGPR write and the writelane
+// (the inline-asm form of round 3 lacked it and produced wrong words)
+__device__ int acoss_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+#endif
+
 namespace acoss {
 
 namespace {
@@ -562,6 +569,52 @@ struct Line {
   __device__ __forceinline__ unsigned min_greater_lane(unsigned x) const { return swar_min_greater(pv, x); }
   __device__ __forceinline__ unsigned min_greater(unsigned x) const { return wave_min_u32(min_greater_lane(x)); }
   static constexpr int kHalves = 1;
+#ifndef ACOSS_NO_HIST_LONG
+  // LineS::hist_rank for the 32 elements per lane of a long line (ACOSS_NO_HIST_LONG: the search
+  // alone, for A/B)
+  static constexpr bool kHist = true;
+  __device__ __forceinline__ bool hist_rank(unsigned hint, int rho, unsigned* hist, unsigned* P, int* le,
+                                            int* less, unsigned* hbase) const {
+    const int lane = threadIdx.x & 63;
+    const unsigned base = hint > 64u ? hint - 64u : 0u;
+    *hbase = base;
+    reinterpret_cast<uint2*>(hist)[lane] = make_uint2(0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    unsigned below = 0;
+    if (base > 0u) {
+      const unsigned X2 = (base - 1u + 0x8000u) * 0x10001u;
+#pragma unroll
+      for (int h = 0; h < KPL / 2; ++h) below = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + below;
+    }
+#pragma unroll
+    for (int h = 0; h < KPL / 2; ++h) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const unsigned c = (half ? (pv[h] >> 16) : (pv[h] & 0xffffu)) - base;
+        if (c < 128u) __hip_atomic_fetch_add(hist + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      }
+    }
+    const int below_tot = wave_sum((int)below);
+    __builtin_amdgcn_wave_barrier();
+    const uint2 hv = reinterpret_cast<const uint2*>(hist)[lane];
+    const int sl = (int)(hv.x + hv.y);
+    const int S = wave_incl_scan(sl);
+    const int tot = __builtin_amdgcn_readlane(S, 63);
+    const int r = rho - below_tot;
+    if (r < 0 || r >= tot) return false;
+    const int E = S - sl;
+    const int src = __builtin_ctzll(__ballot(E <= r && r < S));
+    const int Es = __builtin_amdgcn_readlane(E, src);
+    const int h0 = __builtin_amdgcn_readlane((int)hv.x, src), h1 = __builtin_amdgcn_readlane((int)hv.y, src);
+    const bool second = r >= Es + h0;
+    *P = base + 2u * (unsigned)src + (second ? 1u : 0u);
+    *less = below_tot + Es + (second ? h0 : 0);
+    *le = *less + (second ? h1 : h0);
+    return true;
+  }
+#else
+  static constexpr bool kHist = false;
+#endif
 };
 
 // Short lines (up to 64 KQ elements): lane l holds elements l + 64 q, q < KQ,
@@ -705,12 +758,73 @@ struct LineS {
     *mx = m ? m - 1 : 0u;
   }
   __device__ __forceinline__ unsigned min_greater(unsigned x) const { return wave_min_u32(swar_min_greater(pv, x)); }
+  // Prefix of rank rho (0-based: the least P with count(<= P) > rho) from ONE pass over the line:
+  // every element inside the 128-prefix window [base, base + 128) around the hint (the previous
+  // line's answer; adjacent lines share 8 of their 9 stacked frames, so the answer lies inside
+  // the window for about 99 % of the lines) is counted into its LDS bin, the elements below the
+  // window by one SWAR count; one wave scan of the bins then places rank rho. Two wave reductions
+  // instead of the search's ~5 dependent count passes. Returns false, deciding nothing, when the
+  // answer lies outside the window. le / less: count(<= P) / count(< P), as prefix_of_rank.
+  static constexpr bool kHist = true;
+  __device__ __forceinline__ bool hist_rank(unsigned hint, int rho, unsigned* hist, unsigned* P, int* le,
+                                            int* less, unsigned* hbase) const {
+    const int lane = threadIdx.x & 63;
+    const unsigned base = hint > 64u ? hint - 64u : 0u;
+    *hbase = base;
+    reinterpret_cast<uint2*>(hist)[lane] = make_uint2(0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    // elements below the window (kNone never is): #(prefix <= base - 1), SWAR as count_le
+    unsigned below = 0;
+    if (base > 0u) {
+      const unsigned X2 = (base - 1u + 0x8000u) * 0x10001u;
+#pragma unroll
+      for (int h = 0; h < KQ / 2; ++h) below = __builtin_popcount((X2 - pv[h]) & 0x80008000u) + below;
+    }
+#pragma unroll
+    for (int h = 0; h < KQ / 2; ++h) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const unsigned p = half ? (pv[h] >> 16) : (pv[h] & 0xffffu);
+        // (wraps for p < base; kNone, 0x7fff, is never inside: base <= 0x7f80 - 64)
+        const unsigned c = p - base;
+        if (c < 128u) __hip_atomic_fetch_add(hist + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      }
+    }
+    const int below_tot = wave_sum((int)below);
+    __builtin_amdgcn_wave_barrier();
+    const uint2 hv = reinterpret_cast<const uint2*>(hist)[lane];
+    const int sl = (int)(hv.x + hv.y);
+    const int S = wave_incl_scan(sl);
+    const int tot = __builtin_amdgcn_readlane(S, 63);
+    const int r = rho - below_tot;
+    if (r < 0 || r >= tot) return false;  // wave-uniform: the answer is outside the window
+    const int E = S - sl;
+    const int src = __builtin_ctzll(__ballot(E <= r && r < S));
+    const int Es = __builtin_amdgcn_readlane(E, src);
+    const int h0 = __builtin_amdgcn_readlane((int)hv.x, src), h1 = __builtin_amdgcn_readlane((int)hv.y, src);
+    const bool second = r >= Es + h0;
+    *P = base + 2u * (unsigned)src + (second ? 1u : 0u);
+    *less = below_tot + Es + (second ? h0 : 0);
+    *le = *less + (second ? h1 : h0);
+    return true;
+  }
 };
 
 // Lane t's 32-bit line word t (elements 32 t .. 32 t + 31) from a short line's per-lane mask:
 // word 2q + half is the low / high half of the ballot of bit q. Lanes past 2 KQ get 0.
 template <int KQ>
 __device__ __forceinline__ uint32_t lane_words(uint32_t mask) {
+#ifndef ACOSS_LW_SELECT
+  // each ballot half is wave-uniform (an SGPR): one v_writelane_b32 places it on its lane
+  uint32_t out = 0;
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    const unsigned long long bal = __ballot((mask >> LineS<KQ>::bit_of_q(q)) & 1u);
+    out = (uint32_t)acoss_writelane((int)(uint32_t)bal, 2 * q, (int)out);
+    out = (uint32_t)acoss_writelane((int)(uint32_t)(bal >> 32), 2 * q + 1, (int)out);
+  }
+  return out;
+#else
   const int lane = threadIdx.x & 63;
   uint32_t out = 0;
 #pragma unroll
@@ -720,6 +834,7 @@ __device__ __forceinline__ uint32_t lane_words(uint32_t mask) {
     out = (lane >> 1) == q ? w : out;
   }
   return out;
+#endif
 }
 
 // Lines of 2049..4096 codes: two long-line halves held by one wave, elements [0, 2048) in A
@@ -728,6 +843,7 @@ __device__ __forceinline__ uint32_t lane_words(uint32_t mask) {
 struct Line2 {
   Line<32> A, B;
   static constexpr int kHalves = 2;
+  static constexpr bool kHist = false;
   __device__ __forceinline__ int ebase() const { return A.ebase(); }
   __device__ __forceinline__ int elem(int eb, int b) const { return b < 32 ? eb + b : 2048 + eb + (b - 32); }
   static __device__ __forceinline__ int lane_of(int e) { return e < 2048 ? (e >> 5) : 64 + ((e - 2048) >> 5); }
@@ -881,10 +997,30 @@ __device__ __forceinline__ unsigned sample_hint(const LT& L, int n, float kappa)
   return lo > 0x7f80u ? 0x7f80u : lo;
 }
 
+// The least prefix above P that has elements, and their count, from the bins hist_rank left in
+// LDS (window [base, base + 128)); false when no bin above P inside the window has any.
+__device__ __forceinline__ bool hist_next(const unsigned* hist, unsigned base, unsigned P, unsigned* Pn, int* cnt) {
+  const int lane = threadIdx.x & 63;
+  const uint2 hv = reinterpret_cast<const uint2*>(hist)[lane];
+  const unsigned b0 = base + 2u * (unsigned)lane;
+  const bool n0 = hv.x != 0u && b0 > P, n1 = hv.y != 0u && b0 + 1u > P;
+  const unsigned long long m = __ballot(n0 || n1);
+  if (!m) return false;
+  const int src = __builtin_ctzll(m);
+  const unsigned x = (unsigned)__builtin_amdgcn_readlane((int)hv.x, src);
+  const unsigned y = (unsigned)__builtin_amdgcn_readlane((int)hv.y, src);
+  const unsigned c0 = base + 2u * (unsigned)src;
+  const bool first = x != 0u && c0 > P;
+  *Pn = first ? c0 : c0 + 1u;
+  *cnt = (int)(first ? x : y);
+  return true;
+}
+
 // Scratch of one wave in LDS: element list and 64 bit-words.
-struct WaveLds {
+struct alignas(16) WaveLds {
   int list[64];
   uint32_t words[128];  // le words (64 per line half)
+  uint32_t hist[128];   // the short lines' prefix histogram (LineS::hist_rank)
   float gv[64 * kMS];  // Gram terms of a group's cells, [member][frame]
 };
 
@@ -1083,7 +1219,14 @@ __device__ __forceinline__ void line_threshold(const LT& L, int n, float kappa, 
     asm volatile("" ::"s"(P2), "s"(le2), "s"(less2));
   }
 #endif
-  const unsigned Pl = prefix_of_rank(L, lo, kmin, kmax, n, hint->P, &le, &less, &passes);
+  unsigned Pl = 0u, hbase = 0u;
+  bool found = false;
+#ifndef ACOSS_NO_HIST_SEARCH
+  if constexpr (LT::kHist) {
+    if (hinted) found = L.hist_rank(hint->P, lo, W.hist, &Pl, &le, &less, &hbase);
+  }
+#endif
+  if (!found) Pl = prefix_of_rank(L, lo, kmin, kmax, n, hint->P, &le, &less, &passes);
   ACOSS_STAMP(ts1);
   ACOSS_STAMP_ADD(KF::kRow ? 36 : 32, ts0, ts1);  // prefix search
   ACOSS_COUNT(KF::kRow ? 6 : 11, 1);
@@ -1119,8 +1262,14 @@ __device__ __forceinline__ void line_threshold(const LT& L, int n, float kappa, 
     if (hi < le) {
       vhi = rank_in_prefix(L, Pl, hi - less, le - less, keyf, W, c_lo);
     } else {
-      const unsigned Ph = L.min_greater(Pl);
-      vhi = rank_in_prefix(L, Ph, 0, L.count_le(Ph) - le, keyf, W, c_hi);
+      unsigned Ph;
+      int gh;
+      // the next group from the histogram's bins when the search used one, else two counts
+      if (!(found && hist_next(W.hist, hbase, Pl, &Ph, &gh))) {
+        Ph = L.min_greater(Pl);
+        gh = L.count_le(Ph) - le;
+      }
+      vhi = rank_in_prefix(L, Ph, 0, gh, keyf, W, c_hi);
     }
   }
   ACOSS_STAMP(ts2);
