@@ -377,6 +377,51 @@ __device__ __forceinline__ uint32_t gather_flags8(uint32_t acc, uint32_t s, int 
   return ((s >> (7 - h)) & (0x01010101u << h)) | acc;
 }
 
+// The rank search of hist_rank on a line's 7-bit window codes (w8: four codes per word; window
+// base8 = hint - 63, code c <-> prefix base8 + c exactly for c in 1..126, and for c = 0 too when
+// base8 = 0; code 0 otherwise means "at or below base8", 127 "at or above base8 + 127"): the
+// elements below the window are the zero codes (one SWAR count, 3 VALU per word), every exact
+// code is counted into its LDS bin straight from its byte, and one wave scan of the bins places
+// rank rho. False when the answer is not an exact code.
+template <int NW>
+__device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned base8, int rho, unsigned* hist,
+                                             unsigned* P, int* le, int* less) {
+  const int lane = threadIdx.x & 63;
+  reinterpret_cast<uint2*>(hist)[lane] = make_uint2(0u, 0u);
+  __builtin_amdgcn_wave_barrier();
+  unsigned below = 0;
+  const unsigned cmin = base8 == 0u ? 0u : 1u;  // code 0 is exact only when base8 == 0
+  if (cmin) {
+#pragma unroll
+    for (int h = 0; h < NW; ++h) below = __builtin_popcount((0x80808080u - w8[h]) & 0x80808080u) + below;
+  }
+#pragma unroll
+  for (int h = 0; h < NW; ++h) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned c = (w8[h] >> (8 * k)) & 0x7fu;
+      if (c - cmin < 127u - cmin) __hip_atomic_fetch_add(hist + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+  }
+  const int below_tot = wave_sum((int)below);
+  __builtin_amdgcn_wave_barrier();
+  const uint2 hv = reinterpret_cast<const uint2*>(hist)[lane];
+  const int sl = (int)(hv.x + hv.y);
+  const int S = wave_incl_scan(sl);
+  const int tot = __builtin_amdgcn_readlane(S, 63);
+  const int r = rho - below_tot;
+  if (r < 0 || r >= tot) return false;
+  const int E = S - sl;
+  const int src = __builtin_ctzll(__ballot(E <= r && r < S));
+  const int Es = __builtin_amdgcn_readlane(E, src);
+  const int h0 = __builtin_amdgcn_readlane((int)hv.x, src), h1 = __builtin_amdgcn_readlane((int)hv.y, src);
+  const bool second = r >= Es + h0;
+  *P = base8 + 2u * (unsigned)src + (second ? 1u : 0u);
+  *less = below_tot + Es + (second ? h0 : 0);
+  *le = *less + (second ? h1 : h0);
+  return true;
+}
+
 template <int KPL>
 struct Line {
   static_assert(KPL == 32, "split word order assumes 32 elements per lane");
@@ -575,6 +620,12 @@ struct Line {
   static constexpr bool kHist = true;
   __device__ __forceinline__ bool hist_rank(unsigned hint, int rho, unsigned* hist, unsigned* P, int* le,
                                             int* less, unsigned* hbase) const {
+#ifndef ACOSS_HIST_PV  // (A/B: ACOSS_HIST_PV bins the 16-bit prefixes instead)
+    if (win) {  // the window codes around the same hint (built before every hinted search)
+      *hbase = base8;
+      return hist_rank_w8(w8, base8, rho, hist, P, le, less);
+    }
+#endif
     const int lane = threadIdx.x & 63;
     const unsigned base = hint > 64u ? hint - 64u : 0u;
     *hbase = base;
@@ -768,6 +819,14 @@ struct LineS {
   static constexpr bool kHist = true;
   __device__ __forceinline__ bool hist_rank(unsigned hint, int rho, unsigned* hist, unsigned* P, int* le,
                                             int* less, unsigned* hbase) const {
+#ifndef ACOSS_HIST_PV
+    if constexpr (kWin) {
+      if (win) {
+        *hbase = base8;
+        return hist_rank_w8(w8, base8, rho, hist, P, le, less);
+      }
+    }
+#endif
     const int lane = threadIdx.x & 63;
     const unsigned base = hint > 64u ? hint - 64u : 0u;
     *hbase = base;

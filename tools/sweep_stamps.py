@@ -1,7 +1,7 @@
 """Diagnostic: per-phase s_memtime sums of the fused sweep (k_sweep_rows9) and the column
 select (k_sel_cols9), per wave / per line.
 Needs a build with -DACOSS_STAMPS: bash tools/abbuild.sh stamps -DACOSS_STAMPS, then
-ACOSS_HIP_LIB=tools/abl/libabl_stamps.so python tools/sweep_stamps.py"""
+ACOSS_HIP_LIB=tools/abl/libabl_stamps.so python tools/sweep_stamps.py [frames]"""
 import ctypes
 import os
 import sys
@@ -15,8 +15,9 @@ from acoss import _lib  # noqa: E402
 from acoss.engine import ChromaBank  # noqa: E402
 from bench import corpus_tracks  # noqa: E402
 
+FRAMES = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
 lib = _lib.load_library()
-tracks, _ = corpus_tracks(1, 2000, 20250101)
+tracks, _ = corpus_tracks(1, FRAMES, 20250101)
 bank = ChromaBank(tracks)
 T = len(tracks)
 pairs = torch.as_tensor(np.array([(i, j) for i in range(T) for j in range(i + 1, T)], np.int32)[:4000]).cuda()
