@@ -620,7 +620,7 @@ struct Line {
   static constexpr bool kHist = true;
   __device__ __forceinline__ bool hist_rank(unsigned hint, int rho, unsigned* hist, unsigned* P, int* le,
                                             int* less, unsigned* hbase) const {
-#ifndef ACOSS_HIST_PV  // (A/B: ACOSS_HIST_PV bins the 16-bit prefixes instead)
+#ifdef ACOSS_HIST_W8  // (A/B until measured: bin the window codes instead of the 16-bit prefixes)
     if (win) {  // the window codes around the same hint (built before every hinted search)
       *hbase = base8;
       return hist_rank_w8(w8, base8, rho, hist, P, le, less);
@@ -819,7 +819,7 @@ struct LineS {
   static constexpr bool kHist = true;
   __device__ __forceinline__ bool hist_rank(unsigned hint, int rho, unsigned* hist, unsigned* P, int* le,
                                             int* less, unsigned* hbase) const {
-#ifndef ACOSS_HIST_PV
+#ifdef ACOSS_HIST_W8
     if constexpr (kWin) {
       if (win) {
         *hbase = base8;
@@ -1135,8 +1135,39 @@ __device__ __forceinline__ Group group_keys(const LT& L, unsigned P, int g, cons
   return G;
 }
 
+// Keys of a batched group of at most 16 members sorted ascending across lanes 0..15 (lanes >= g
+// hold 0xffffffff, above every real key, so they sort last): the all-ascending bitonic network
+// (per block size k: the mirror step, then the xor half-cleaners), every partner fetched by DPP
+// inside the 16-lane row, min to the lower lane. 10 steps of about 3 VALU, against about 10
+// instructions per member for the counting loop below (A/B until measured: ACOSS_RANK_SORT16).
+template <int CTRL>
+__device__ __forceinline__ unsigned cx_dpp(unsigned v, int lane, int m) {
+  const unsigned p = dpp_u32<CTRL>(v, v);
+  return (lane & m) ? max(v, p) : min(v, p);
+}
+__device__ __forceinline__ unsigned sort16_lanes(unsigned v) {
+  const int lane = threadIdx.x & 15;
+  v = cx_dpp<0xB1>(v, lane, 1);   // k = 2: lanes l ^ 1
+  v = cx_dpp<0x1B>(v, lane, 2);   // k = 4: mirror within 4 (quad_perm 3,2,1,0)
+  v = cx_dpp<0xB1>(v, lane, 1);
+  v = cx_dpp<0x141>(v, lane, 4);  // k = 8: row_half_mirror
+  v = cx_dpp<0x4E>(v, lane, 2);   //        l ^ 2 (quad_perm 2,3,0,1)
+  v = cx_dpp<0xB1>(v, lane, 1);
+  v = cx_dpp<0x140>(v, lane, 8);  // k = 16: row_mirror
+  {                               //         l ^ 4: row_shl:4 below, row_shr:4 above
+    const unsigned up = dpp_u32<0x104>(v, v), dn = dpp_u32<0x114>(v, v);
+    v = (lane & 4) ? max(v, dn) : min(v, up);
+  }
+  v = cx_dpp<0x4E>(v, lane, 2);
+  v = cx_dpp<0xB1>(v, lane, 1);
+  return v;
+}
+
 // Key of rank rho (0-based) inside a batched group.
 __device__ __forceinline__ unsigned group_rank(const Group& G, int rho) {
+#ifdef ACOSS_RANK_SORT16
+  if (G.g <= 16) return (unsigned)__builtin_amdgcn_readlane((int)sort16_lanes(G.key), rho);
+#endif
   const int lane = threadIdx.x & 63;
   int cl = 0, ce = 0;
   for (int k = 0; k < G.g; ++k) {
@@ -1151,6 +1182,14 @@ __device__ __forceinline__ unsigned group_rank(const Group& G, int rho) {
 
 // Keys of ranks rho and rho + 1 inside a batched group (rho + 1 < g), one counting loop.
 __device__ __forceinline__ void group_rank2(const Group& G, int rho, unsigned* v0, unsigned* v1) {
+#ifdef ACOSS_RANK_SORT16
+  if (G.g <= 16) {
+    const unsigned srt = sort16_lanes(G.key);
+    *v0 = (unsigned)__builtin_amdgcn_readlane((int)srt, rho);
+    *v1 = (unsigned)__builtin_amdgcn_readlane((int)srt, rho + 1);
+    return;
+  }
+#endif
   const int lane = threadIdx.x & 63;
   int cl = 0, ce = 0;
   for (int k = 0; k < G.g; ++k) {
