@@ -475,7 +475,14 @@ struct Line {
     unsigned w[KPL / 2];
 #pragma unroll
     for (int q = 0; q < KPL / 8; ++q) {
+#ifdef ACOSS_HC_NTLOAD  // column plane read once: streaming loads, so they do not evict the frames from L2
+      typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+      const u32x4v vv = STORED_SPLIT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(src) + q)
+                                     : reinterpret_cast<const u32x4v*>(src)[q];
+      const uint4 v = make_uint4(vv.x, vv.y, vv.z, vv.w);
+#else
       const uint4 v = reinterpret_cast<const uint4*>(src)[q];
+#endif
       w[4 * q + 0] = v.x;
       w[4 * q + 1] = v.y;
       w[4 * q + 2] = v.z;
@@ -620,7 +627,7 @@ struct Line {
   static constexpr bool kHist = true;
   __device__ __forceinline__ bool hist_rank(unsigned hint, int rho, unsigned* hist, unsigned* P, int* le,
                                             int* less, unsigned* hbase) const {
-#ifdef ACOSS_HIST_W8  // (A/B until measured: bin the window codes instead of the 16-bit prefixes)
+#ifndef ACOSS_HIST_PV  // (ACOSS_HIST_PV: bin the 16-bit prefixes instead, for A/B)
     if (win) {  // the window codes around the same hint (built before every hinted search)
       *hbase = base8;
       return hist_rank_w8(w8, base8, rho, hist, P, le, less);
@@ -819,7 +826,7 @@ struct LineS {
   static constexpr bool kHist = true;
   __device__ __forceinline__ bool hist_rank(unsigned hint, int rho, unsigned* hist, unsigned* P, int* le,
                                             int* less, unsigned* hbase) const {
-#ifdef ACOSS_HIST_W8
+#ifndef ACOSS_HIST_PV
     if constexpr (kWin) {
       if (win) {
         *hbase = base8;
@@ -1088,8 +1095,10 @@ struct alignas(16) WaveLds {
 struct Group {
   unsigned P;
   int g;
-  int elem;      // this lane's element (lane < g)
-  unsigned key;  // its exact key (0xffffffff for lane >= g)
+  int elem;      // this lane's element (lanes off .. off + g - 1)
+  unsigned key;  // its exact key (0xffffffff on lanes without a member)
+  int off;       // first lane of the group's members (0, or g1 for the second group of group_keys2)
+  __device__ __forceinline__ bool mine(int lane) const { return (unsigned)(lane - off) < (unsigned)g; }
 };
 
 template <class LT, class KF>
@@ -1122,6 +1131,7 @@ __device__ __forceinline__ Group group_keys(const LT& L, unsigned P, int g, cons
   Group G;
   G.P = P;
   G.g = g;
+  G.off = 0;
   G.elem = lane < g ? e_me : 0;
   G.key = 0xffffffffu;
   if (lane < g) {
@@ -1135,11 +1145,67 @@ __device__ __forceinline__ Group group_keys(const LT& L, unsigned P, int g, cons
   return G;
 }
 
+// The exact keys of TWO prefix groups in one batched pass (the lower order statistic's group P1
+// and, when the upper one is the least key of the next non-empty prefix P2, that group): one
+// packed scan for both member lists, then the same rounds over 9 (g1 + g2) Gram terms. Members
+// of P1 on lanes [0, g1), of P2 on lanes [g1, g1 + g2); g1 + g2 <= 64. One recompute round trip
+// instead of two for the ~28 % of lines whose two order statistics straddle a prefix boundary.
+template <class LT, class KF>
+__device__ __forceinline__ void group_keys2(const LT& L, unsigned P1, int g1, unsigned P2, int g2, const KF& keyf,
+                                            WaveLds& W, Group* G1, Group* G2) {
+  const int lane = threadIdx.x & 63;
+  const int ebase = L.ebase();
+  auto m1 = L.eq_mask(P1);
+  auto m2 = L.eq_mask(P2);
+  const int c1 = popc(m1), c2 = popc(m2);
+  const int packed = c1 | (c2 << 16);  // per-lane counts <= 64: one scan for both lists
+  const int sc = wave_incl_scan(packed) - packed;
+  int i1 = sc & 0xffff, i2 = g1 + (sc >> 16);
+  while (m1) {
+    W.list[i1++] = L.elem(ebase, ctz(m1));
+    m1 &= m1 - 1;
+  }
+  while (m2) {
+    W.list[i2++] = L.elem(ebase, ctz(m2));
+    m2 &= m2 - 1;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int g = g1 + g2;
+  const int e_me = W.list[lane < g ? lane : 0];
+  const float nq_me = keyf.V.NXq[keyf.qi(e_me)], nr_me = keyf.V.NXr[keyf.rj(e_me)];
+  for (int t = lane; t < kMS * g; t += 64) {
+    const int k = t / kMS, u = t - k * kMS;
+    const int e = W.list[k];
+    W.gv[t] = cell_gram(keyf.V, (keyf.qi(e) + u) * keyf.V.tau, (keyf.rj(e) + u) * keyf.V.tau);
+  }
+  __builtin_amdgcn_wave_barrier();
+  ACOSS_COUNT(KF::kRow ? 8 : 13, 1);
+  ACOSS_COUNT(KF::kRow ? 9 : 14, g);
+  unsigned key = 0xffffffffu;
+  if (lane < g) {
+    float dot = W.gv[lane * kMS];
+#pragma unroll
+    for (int u = 1; u < kMS; ++u) dot = dot + W.gv[lane * kMS + u];
+    const float d2 = (nq_me - 2.0f * dot) + nr_me;
+    key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int elem = lane < g ? e_me : 0;
+  *G1 = Group{P1, g1, elem, lane < g1 ? key : 0xffffffffu, 0};
+  *G2 = Group{P2, g2, elem, (lane >= g1 && lane < g) ? key : 0xffffffffu, g1};
+}
+
+// Least key of a batched group (its rank 0), one wave minimum.
+__device__ __forceinline__ unsigned group_min(const Group& G) {
+  return wave_min_u32(G.mine(threadIdx.x & 63) ? G.key : 0xffffffffu);
+}
+
 // Keys of a batched group of at most 16 members sorted ascending across lanes 0..15 (lanes >= g
 // hold 0xffffffff, above every real key, so they sort last): the all-ascending bitonic network
 // (per block size k: the mirror step, then the xor half-cleaners), every partner fetched by DPP
 // inside the 16-lane row, min to the lower lane. 10 steps of about 3 VALU, against about 10
-// instructions per member for the counting loop below (A/B until measured: ACOSS_RANK_SORT16).
+// instructions per member for the counting loop below, so it is used from 6 members on (A/B until
+// measured: ACOSS_RANK_SORT16).
 template <int CTRL>
 __device__ __forceinline__ unsigned cx_dpp(unsigned v, int lane, int m) {
   const unsigned p = dpp_u32<CTRL>(v, v);
@@ -1163,10 +1229,10 @@ __device__ __forceinline__ unsigned sort16_lanes(unsigned v) {
   return v;
 }
 
-// Key of rank rho (0-based) inside a batched group.
+// Key of rank rho (0-based) inside a batched group whose members start at lane 0 (off == 0).
 __device__ __forceinline__ unsigned group_rank(const Group& G, int rho) {
 #ifdef ACOSS_RANK_SORT16
-  if (G.g <= 16) return (unsigned)__builtin_amdgcn_readlane((int)sort16_lanes(G.key), rho);
+  if (G.g >= 6 && G.g <= 16) return (unsigned)__builtin_amdgcn_readlane((int)sort16_lanes(G.key), rho);
 #endif
   const int lane = threadIdx.x & 63;
   int cl = 0, ce = 0;
@@ -1183,7 +1249,7 @@ __device__ __forceinline__ unsigned group_rank(const Group& G, int rho) {
 // Keys of ranks rho and rho + 1 inside a batched group (rho + 1 < g), one counting loop.
 __device__ __forceinline__ void group_rank2(const Group& G, int rho, unsigned* v0, unsigned* v1) {
 #ifdef ACOSS_RANK_SORT16
-  if (G.g <= 16) {
+  if (G.g >= 6 && G.g <= 16) {
     const unsigned srt = sort16_lanes(G.key);
     *v0 = (unsigned)__builtin_amdgcn_readlane((int)srt, rho);
     *v1 = (unsigned)__builtin_amdgcn_readlane((int)srt, rho + 1);
@@ -1344,19 +1410,31 @@ __device__ __forceinline__ void line_threshold(const LT& L, int n, float kappa, 
   // density around the answer: the group at Pl, smoothed over the run
   hint->dens = hinted ? 0.5f * hint->dens + 0.5f * (float)(le - less) : (float)(le - less);
   unsigned vlo, vhi;
+  unsigned Ph2 = 0u;
+  int gh2 = 0;
+  const bool straddle = hi != lo && hi >= le && le - less <= 64;  // the upper statistic: least key above Pl
+#if !defined(ACOSS_NO_GROUP2) && !defined(ACOSS_ABL_NOGROUP) && !defined(ACOSS_ABL_NOGROUP2)
+  const bool both = straddle && found && hist_next(W.hist, hbase, Pl, &Ph2, &gh2) && (le - less) + gh2 <= 64;
+#else
+  const bool both = false;
+#endif
 #if defined(ACOSS_ABL_NOGROUP) || defined(ACOSS_ABL_NOGROUP2)
   if (true) {
     vlo = vhi = Pl << 16;
   } else
 #endif
-  if (hi != lo && hi < le && le - less <= 64) {
+  if (both) {
+    group_keys2(L, Pl, le - less, Ph2, gh2, keyf, W, c_lo, c_hi);
+    vlo = group_rank(*c_lo, lo - less);
+    vhi = group_min(*c_hi);
+  } else if (hi != lo && hi < le && le - less <= 64) {
     *c_lo = group_keys(L, Pl, le - less, keyf, W);
     group_rank2(*c_lo, lo - less, &vlo, &vhi);
   } else {
     vlo = rank_in_prefix(L, Pl, lo - less, le - less, keyf, W, c_lo);
     vhi = vlo;
   }
-  if (hi != lo && !(hi < le && le - less <= 64)) {
+  if (!both && hi != lo && !(hi < le && le - less <= 64)) {
     if (hi < le) {
       vhi = rank_in_prefix(L, Pl, hi - less, le - less, keyf, W, c_lo);
     } else {
@@ -1407,10 +1485,10 @@ __device__ __forceinline__ auto le_bits(const LT& L, unsigned Tbits, const KF& k
   if (LT::kHalves == 2) W.words[64 + lane] = 0xffffffffu;
   __builtin_amdgcn_wave_barrier();
   if (lo_hit || hi_hit) {
-    const int cg = lo_hit ? c_lo.g : c_hi.g;
+    const bool cmine = lo_hit ? c_lo.mine(lane) : c_hi.mine(lane);
     const unsigned ckey = lo_hit ? c_lo.key : c_hi.key;
     const int celem = lo_hit ? c_lo.elem : c_hi.elem;
-    if (lane < cg && ckey > Tbits) atomicAnd(&W.words[LT::lane_of(celem)], ~(1u << LT::bit_of(celem)));
+    if (cmine && ckey > Tbits) atomicAnd(&W.words[LT::lane_of(celem)], ~(1u << LT::bit_of(celem)));
   } else {
     const int g = wave_sum(popc(L.eq_mask(T16)));
     if (g == 0) return word;
@@ -1681,7 +1759,15 @@ template <int KQ>
 __global__ __launch_bounds__(kThreads, ACOSS_SWEEP_WPE) void k_sweep_rows9(SweepArgs A) {
   __shared__ __attribute__((aligned(16))) char smem[kSweepLds<KQ>];
   __shared__ int s_slot;
+#ifdef ACOSS_SWEEP_XCD
+  // all strips of a pair on one XCD (its L2 then holds the pair's frames for the walk and for the
+  // row select's exact-key recompute)
+  const int nblk = gridDim.x * gridDim.y;
+  const int lb = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, nblk);
+  sweep_rows_block<KQ>(A, lb % gridDim.x, lb / gridDim.x, smem, &s_slot);
+#else
   sweep_rows_block<KQ>(A, blockIdx.x, blockIdx.y, smem, &s_slot);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
