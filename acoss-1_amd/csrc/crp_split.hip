@@ -101,13 +101,8 @@ struct KeyPlanes {
 // Exact key of cell (i, j), recomputed in the sweep's canonical order: 12-term fmaf chain per
 // frame pair (cell_gram), sequential 9-term sum, d2 = (NX_i - 2 dot) + NY_j clamped at +0
 // (cell_finish). Valid cells only (i < M', j < N'): every frame is inside its track.
-__device__ __forceinline__ float cell_gram(const PairView& V, int fq, int fr) {
-#ifdef ACOSS_ABL_NOGRAM  // timing ablation only (wrong results): no frame loads in the recompute
-  return (float)(fq * 3 + fr);
-#endif
-  const f32x4* x = reinterpret_cast<const f32x4*>(V.X + (size_t)fq * 12);
-  const f32x4* y = reinterpret_cast<const f32x4*>(V.Yr + (size_t)fr * 12);
-  const f32x4 x0 = x[0], x1 = x[1], x2 = x[2], y0 = y[0], y1 = y[1], y2 = y[2];
+__device__ __forceinline__ float gram12(const f32x4& x0, const f32x4& x1, const f32x4& x2, const f32x4& y0,
+                                        const f32x4& y1, const f32x4& y2) {
   float g = 0.0f;
   g = __builtin_fmaf(x0.x, y0.x, g);
   g = __builtin_fmaf(x0.y, y0.y, g);
@@ -122,6 +117,16 @@ __device__ __forceinline__ float cell_gram(const PairView& V, int fq, int fr) {
   g = __builtin_fmaf(x2.z, y2.z, g);
   g = __builtin_fmaf(x2.w, y2.w, g);
   return g;
+}
+
+__device__ __forceinline__ float cell_gram(const PairView& V, int fq, int fr) {
+#ifdef ACOSS_ABL_NOGRAM  // timing ablation only (wrong results): no frame loads in the recompute
+  return (float)(fq * 3 + fr);
+#endif
+  const f32x4* x = reinterpret_cast<const f32x4*>(V.X + (size_t)fq * 12);
+  const f32x4* y = reinterpret_cast<const f32x4*>(V.Yr + (size_t)fr * 12);
+  const f32x4 x0 = x[0], x1 = x[1], x2 = x[2], y0 = y[0], y1 = y[1], y2 = y[2];
+  return gram12(x0, x1, x2, y0, y1, y2);
 }
 
 __device__ __forceinline__ unsigned cell_finish(const PairView& V, int i, int j, float dot) {
@@ -1360,14 +1365,25 @@ __device__ __forceinline__ unsigned rank_in_prefix(const LT& L, unsigned P, int 
   return big_group_rank(L, P, rho, g, keyf, W);
 }
 
-// Threshold (distance units) and squared-domain threshold of a line of n keys; leaves the
-// exact keys of the last batched group in *cache for le_bits.
+// The search half of a line's threshold: the rank targets lo / hi of the percentile, the prefix
+// Pl of rank lo with count(<= Pl) = le and count(< Pl) = less, and, when the two order statistics
+// straddle a prefix boundary and the histogram holds it, the next group (Ph2, gh2).
+struct Plan {
+  unsigned Pl, hbase, Ph2;
+  int le, less, gh2, lo, hi;
+  float q, lo_f, hi_f;
+  bool found, next_ok, both;  // next_ok: (Ph2, gh2) = the next group, read from the histogram
+};
+
 template <class LT, class KF>
-__device__ __forceinline__ void line_threshold(const LT& L, int n, float kappa, const KF& keyf, WaveLds& W, Group* c_lo,
-                               Group* c_hi, float* thr, float* T, Hint* hint) {
-  const float q = (float)(n - 1) * kappa;
-  const float lo_f = floorf(q), hi_f = ceilf(q);
-  const int lo = (int)lo_f, hi = (int)hi_f;
+__device__ __forceinline__ Plan line_plan(const LT& L, int n, float kappa, WaveLds& W, Hint* hint) {
+  Plan pl;
+  pl.q = (float)(n - 1) * kappa;
+  pl.lo_f = floorf(pl.q);
+  pl.hi_f = ceilf(pl.q);
+  pl.lo = (int)pl.lo_f;
+  pl.hi = (int)pl.hi_f;
+  const int lo = pl.lo, hi = pl.hi;
   unsigned kmin = 0, kmax = 0x7f80u;  // every real prefix (finite non-negative float) is <= 0x7f80
   const bool hinted = hint->P != kNoHint;
   if (!hinted) L.min_max(&kmin, &kmax);
@@ -1409,22 +1425,40 @@ __device__ __forceinline__ void line_threshold(const LT& L, int n, float kappa, 
   hint->P = Pl;
   // density around the answer: the group at Pl, smoothed over the run
   hint->dens = hinted ? 0.5f * hint->dens + 0.5f * (float)(le - less) : (float)(le - less);
-  unsigned vlo, vhi;
-  unsigned Ph2 = 0u;
-  int gh2 = 0;
-  const bool straddle = hi != lo && hi >= le && le - less <= 64;  // the upper statistic: least key above Pl
+  pl.Pl = Pl;
+  pl.hbase = hbase;
+  pl.le = le;
+  pl.less = less;
+  pl.found = found;
+  pl.Ph2 = 0u;
+  pl.gh2 = 0;
+  // the upper statistic is the least key above Pl: its group from the histogram's bins, read now
+  // (the bins belong to this line only until the next line's search)
+  pl.next_ok = hi != lo && hi >= le && found && hist_next(W.hist, hbase, Pl, &pl.Ph2, &pl.gh2);
 #if !defined(ACOSS_NO_GROUP2) && !defined(ACOSS_ABL_NOGROUP) && !defined(ACOSS_ABL_NOGROUP2)
-  const bool both = straddle && found && hist_next(W.hist, hbase, Pl, &Ph2, &gh2) && (le - less) + gh2 <= 64;
+  pl.both = pl.next_ok && le - less <= 64 && (le - less) + pl.gh2 <= 64;
 #else
-  const bool both = false;
+  pl.both = false;
 #endif
+  return pl;
+}
+
+// The exact values vlo / vhi of the two order statistics from a plan: the groups' keys recomputed
+// (cached in *c_lo / *c_hi for le_bits).
+template <class LT, class KF>
+__device__ __forceinline__ void line_groups(const LT& L, const Plan& pl, const KF& keyf, WaveLds& W, Group* c_lo,
+                                            Group* c_hi, unsigned* vlo_o, unsigned* vhi_o) {
+  const unsigned Pl = pl.Pl;
+  const int le = pl.le, less = pl.less, lo = pl.lo, hi = pl.hi;
+  unsigned vlo, vhi;
+  ACOSS_STAMP(ts1);
 #if defined(ACOSS_ABL_NOGROUP) || defined(ACOSS_ABL_NOGROUP2)
   if (true) {
     vlo = vhi = Pl << 16;
   } else
 #endif
-  if (both) {
-    group_keys2(L, Pl, le - less, Ph2, gh2, keyf, W, c_lo, c_hi);
+  if (pl.both) {
+    group_keys2(L, Pl, le - less, pl.Ph2, pl.gh2, keyf, W, c_lo, c_hi);
     vlo = group_rank(*c_lo, lo - less);
     vhi = group_min(*c_hi);
   } else if (hi != lo && hi < le && le - less <= 64) {
@@ -1434,14 +1468,17 @@ __device__ __forceinline__ void line_threshold(const LT& L, int n, float kappa, 
     vlo = rank_in_prefix(L, Pl, lo - less, le - less, keyf, W, c_lo);
     vhi = vlo;
   }
-  if (!both && hi != lo && !(hi < le && le - less <= 64)) {
+  if (!pl.both && hi != lo && !(hi < le && le - less <= 64)) {
     if (hi < le) {
       vhi = rank_in_prefix(L, Pl, hi - less, le - less, keyf, W, c_lo);
     } else {
       unsigned Ph;
       int gh;
       // the next group from the histogram's bins when the search used one, else two counts
-      if (!(found && hist_next(W.hist, hbase, Pl, &Ph, &gh))) {
+      if (pl.next_ok) {
+        Ph = pl.Ph2;
+        gh = pl.gh2;
+      } else {
         Ph = L.min_greater(Pl);
         gh = L.count_le(Ph) - le;
       }
@@ -1450,20 +1487,35 @@ __device__ __forceinline__ void line_threshold(const LT& L, int n, float kappa, 
   }
   ACOSS_STAMP(ts2);
   ACOSS_STAMP_ADD(KF::kRow ? 37 : 33, ts1, ts2);  // group keys and ranks
+  *vlo_o = vlo;
+  *vhi_o = vhi;
+}
+
+// Percentile threshold (linear interpolation in the sqrt domain) and its squared-domain form.
+__device__ __forceinline__ void plan_threshold(const Plan& pl, unsigned vlo, unsigned vhi, float* thr, float* T) {
   const float slo = sqrt_rn(__builtin_bit_cast(float, vlo));
   float th;
-  if (lo_f == hi_f) {
+  if (pl.lo_f == pl.hi_f) {
     th = slo;
   } else {
     const float shi = sqrt_rn(__builtin_bit_cast(float, vhi));
-    const float aa = slo * (hi_f - q);
-    const float bb = shi * (q - lo_f);
+    const float aa = slo * (pl.hi_f - pl.q);
+    const float bb = shi * (pl.q - pl.lo_f);
     th = aa + bb;
   }
   *thr = th;
   *T = sq_threshold(th);
-  ACOSS_STAMP(ts3);
-  ACOSS_STAMP_ADD(KF::kRow ? 38 : 34, ts2, ts3);  // threshold arithmetic
+}
+
+// Threshold (distance units) and squared-domain threshold of a line of n keys; leaves the
+// exact keys of the last batched group in *cache for le_bits.
+template <class LT, class KF>
+__device__ __forceinline__ void line_threshold(const LT& L, int n, float kappa, const KF& keyf, WaveLds& W, Group* c_lo,
+                               Group* c_hi, float* thr, float* T, Hint* hint) {
+  const Plan pl = line_plan<LT, KF>(L, n, kappa, W, hint);
+  unsigned vlo, vhi;
+  line_groups(L, pl, keyf, W, c_lo, c_hi, &vlo, &vhi);
+  plan_threshold(pl, vlo, vhi, thr, T);
 }
 
 // Bits of "key <= T" for this lane's elements (in the line type's bit order): every
