@@ -1634,7 +1634,11 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
     }
   };
   // Line2 loads each line when it starts (no prefetch: 48 VGPRs, the 4th wave per SIMD)
+#ifdef ACOSS_ROWS_NOPF  // no next-row prefetch (fewer VGPRs: occupancy over latency), for A/B
+  constexpr bool kPF = false;
+#else
   constexpr bool kPF = KQ != 2;
+#endif
   LT Lnext;
   if (kPF && i0 + w * RPW < V.Mp) load_row(Lnext, i0 + w * RPW);
 #pragma unroll 1

@@ -69,7 +69,7 @@ def corpus(n_tracks, frames, seed, kind="hard"):
     return tracks[:n_tracks], np.asarray(labels[:n_tracks], np.int32)
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--algo", choices=["serra09", "simple"], default="serra09")
     ap.add_argument("--tracks", type=int, default=15000)
@@ -81,7 +81,12 @@ def main():
     ap.add_argument("--threads", type=int, default=16, help="CPU oracle threads for the sample")
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--out", default=None)
-    a = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def run(a):
+    """The whole flow for the parsed options `a`; returns the result dict (res["ok"]: every check
+    passed). Also the body of tests/test_gpu_datacos_full.py, at a short frame count."""
     import torch
     import oracle
     from acoss import evaluation, synthetic
@@ -194,6 +199,13 @@ def main():
     algo.cleanup_memmap()
     if not a.workdir:
         shutil.rmtree(work, ignore_errors=True)
+    return res
+
+
+def main():
+    a = parse_args()
+    res = run(a)
+    ok = res["ok"]
     line = json.dumps(res)
     print(line, flush=True)
     if a.out:
