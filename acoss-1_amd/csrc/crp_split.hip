@@ -382,6 +382,29 @@ __device__ __forceinline__ uint32_t gather_flags8(uint32_t acc, uint32_t s, int 
   return ((s >> (7 - h)) & (0x01010101u << h)) | acc;
 }
 
+// One element into the LDS prefix histogram: bin c when `in`, else this lane's own sink word (the
+// 64 words after the 128 bins, WaveLds::sink), so that every element issues the same
+// unconditional ds_add (a lane-private address: no bank conflict) instead of a compare, an exec
+// mask save / restore and a masked add per element (ACOSS_HIST_MASKED: the masked form, for A/B).
+typedef __attribute__((address_space(3))) unsigned lds_u32;
+// 32-bit LDS addresses of a wave's histogram: the bins' base as an SGPR (bin address = c * 4 +
+// base in one v_lshl_add) and this lane's sink word
+struct HistAddr {
+  unsigned hb, sk;
+  __device__ __forceinline__ explicit HistAddr(unsigned* hist) {
+    hb = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(size_t)(lds_u32*)hist);
+    sk = hb + 512u + 4u * (threadIdx.x & 63);
+  }
+};
+__device__ __forceinline__ void hist_add(unsigned* hist, const HistAddr& A, unsigned c, bool in) {
+#ifndef ACOSS_HIST_SINK_PV  // the 16-bit prefix forms keep the masked add (the sink: -6 % at 500 frames)
+  if (in) __hip_atomic_fetch_add(hist + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#else
+  const unsigned a = in ? A.hb + 4u * c : A.sk;
+  __hip_atomic_fetch_add((lds_u32*)(size_t)a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#endif
+}
+
 // The rank search of hist_rank on a line's 7-bit window codes (w8: four codes per word; window
 // base8 = hint - 63, code c <-> prefix base8 + c exactly for c in 1..126, and for c = 0 too when
 // base8 = 0; code 0 otherwise means "at or below base8", 127 "at or above base8 + 127"): the
@@ -400,6 +423,7 @@ __device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned 
 #pragma unroll
     for (int h = 0; h < NW; ++h) below = __builtin_popcount((0x80808080u - w8[h]) & 0x80808080u) + below;
   }
+#ifdef ACOSS_HIST_MASKED
 #pragma unroll
   for (int h = 0; h < NW; ++h) {
 #pragma unroll
@@ -408,6 +432,22 @@ __device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned 
       if (c - cmin < 127u - cmin) __hip_atomic_fetch_add(hist + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
   }
+#else
+  // per code: cm = byte - cmin (one SDWA subtract: codes are 7-bit, so the byte is the code), the
+  // bin address from cm and an SGPR base, the sink for codes outside [cmin, 126]; 4 VALU, no SALU
+  const HistAddr A(hist);
+  const unsigned hb = A.hb + 4u * cmin, sk = A.sk;
+  const unsigned lim = 127u - cmin;
+#pragma unroll
+  for (int h = 0; h < NW; ++h) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned cm = ((w8[h] >> (8 * k)) & 0xffu) - cmin;
+      const unsigned a = cm < lim ? hb + 4u * cm : sk;
+      __hip_atomic_fetch_add((lds_u32*)(size_t)a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+  }
+#endif
   const int below_tot = wave_sum((int)below);
   __builtin_amdgcn_wave_barrier();
   const uint2 hv = reinterpret_cast<const uint2*>(hist)[lane];
@@ -643,6 +683,7 @@ struct Line {
     *hbase = base;
     reinterpret_cast<uint2*>(hist)[lane] = make_uint2(0u, 0u);
     __builtin_amdgcn_wave_barrier();
+    const HistAddr HA(hist);
     unsigned below = 0;
     if (base > 0u) {
       const unsigned X2 = (base - 1u + 0x8000u) * 0x10001u;
@@ -654,7 +695,7 @@ struct Line {
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         const unsigned c = (half ? (pv[h] >> 16) : (pv[h] & 0xffffu)) - base;
-        if (c < 128u) __hip_atomic_fetch_add(hist + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        hist_add(hist, HA, c, c < 128u);
       }
     }
     const int below_tot = wave_sum((int)below);
@@ -844,6 +885,7 @@ struct LineS {
     *hbase = base;
     reinterpret_cast<uint2*>(hist)[lane] = make_uint2(0u, 0u);
     __builtin_amdgcn_wave_barrier();
+    const HistAddr HA(hist);
     // elements below the window (kNone never is): #(prefix <= base - 1), SWAR as count_le
     unsigned below = 0;
     if (base > 0u) {
@@ -858,7 +900,7 @@ struct LineS {
         const unsigned p = half ? (pv[h] >> 16) : (pv[h] & 0xffffu);
         // (wraps for p < base; kNone, 0x7fff, is never inside: base <= 0x7f80 - 64)
         const unsigned c = p - base;
-        if (c < 128u) __hip_atomic_fetch_add(hist + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        hist_add(hist, HA, c, c < 128u);
       }
     }
     const int below_tot = wave_sum((int)below);
@@ -1091,7 +1133,8 @@ __device__ __forceinline__ bool hist_next(const unsigned* hist, unsigned base, u
 struct alignas(16) WaveLds {
   int list[64];
   uint32_t words[128];  // le words (64 per line half)
-  uint32_t hist[128];   // the short lines' prefix histogram (LineS::hist_rank)
+  uint32_t hist[128];   // the lines' prefix histogram (hist_rank)
+  uint32_t sink[64];    // per-lane targets of the elements outside the histogram (hist_add)
   float gv[64 * kMS];  // Gram terms of a group's cells, [member][frame]
 };
 
@@ -1387,7 +1430,7 @@ __device__ __forceinline__ Plan line_plan(const LT& L, int n, float kappa, WaveL
   unsigned kmin = 0, kmax = 0x7f80u;  // every real prefix (finite non-negative float) is <= 0x7f80
   const bool hinted = hint->P != kNoHint;
   if (!hinted) L.min_max(&kmin, &kmax);
-  int le, less;
+  int le = 0, less = 0;
   int passes = 0;
   ACOSS_STAMP(ts0);
 #ifdef ACOSS_ABL_SEARCH2X  // timing ablation only: the search runs twice (same answer)
@@ -1954,7 +1997,7 @@ __device__ __forceinline__ void cols_block(const ColsArgs& A, int lin, int ncb, 
   const PairView V = pair_view(B, p);
   const int j0 = (lb - p * ncb) * kColsPerBlock<KQ> + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kCPW<KQ>;
   const int jend = min(j0 + kCPW<KQ>, V.Np);
-  WaveLds& W = wl[threadIdx.x >> 6];
+  WaveLds& W = wl[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];  // an SGPR base for the LDS addresses
   if (KQ == 8 || V.Mp <= short_n)
     cols_body<8>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
   else if (KQ == 16)
