@@ -407,10 +407,10 @@ __device__ __forceinline__ void hist_add(unsigned* hist, const HistAddr& A, unsi
 
 // The rank search of hist_rank on a line's 7-bit window codes (w8: four codes per word; window
 // base8 = hint - 63, code c <-> prefix base8 + c exactly for c in 1..126, and for c = 0 too when
-// base8 = 0; code 0 otherwise means "at or below base8", 127 "at or above base8 + 127"): the
-// elements below the window are the zero codes (one SWAR count, 3 VALU per word), every exact
-// code is counted into its LDS bin straight from its byte, and one wave scan of the bins places
-// rank rho. False when the answer is not an exact code.
+// base8 = 0; code 0 otherwise means "at or below base8", 127 "at or above base8 + 127"): every
+// code below 127 is counted into its LDS bin straight from its byte (bin 0 then holds the
+// elements at or below base8), and one wave scan of the bins places rank rho. False when the
+// answer is not an exact code (above the window, or in bin 0 of a window above 0).
 template <int NW>
 __device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned base8, int rho, unsigned* hist,
                                              unsigned* P, int* le, int* less) {
@@ -419,11 +419,11 @@ __device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned 
   __builtin_amdgcn_wave_barrier();
   unsigned below = 0;
   const unsigned cmin = base8 == 0u ? 0u : 1u;  // code 0 is exact only when base8 == 0
+#ifdef ACOSS_HIST_MASKED
   if (cmin) {
 #pragma unroll
     for (int h = 0; h < NW; ++h) below = __builtin_popcount((0x80808080u - w8[h]) & 0x80808080u) + below;
   }
-#ifdef ACOSS_HIST_MASKED
 #pragma unroll
   for (int h = 0; h < NW; ++h) {
 #pragma unroll
@@ -432,23 +432,25 @@ __device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned 
       if (c - cmin < 127u - cmin) __hip_atomic_fetch_add(hist + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
   }
+  const int below_tot = wave_sum((int)below);
 #else
-  // per code: cm = byte - cmin (one SDWA subtract: codes are 7-bit, so the byte is the code), the
-  // bin address from cm and an SGPR base, the sink for codes outside [cmin, 126]; 4 VALU, no SALU
+  // every code below 127 into its bin, code 0 included (the elements at or below base8, exact
+  // only when base8 == 0: a rank landing in bin 0 otherwise returns false below), so no separate
+  // count of the elements under the window; code 127 to this lane's sink. Per code: the byte (7-bit
+  // codes: the byte is the code), its bin address from an SGPR base, one select; no exec masking.
   const HistAddr A(hist);
-  const unsigned hb = A.hb + 4u * cmin, sk = A.sk;
-  const unsigned lim = 127u - cmin;
 #pragma unroll
   for (int h = 0; h < NW; ++h) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const unsigned cm = ((w8[h] >> (8 * k)) & 0xffu) - cmin;
-      const unsigned a = cm < lim ? hb + 4u * cm : sk;
+      const unsigned c = (w8[h] >> (8 * k)) & 0xffu;
+      const unsigned a = c < 127u ? A.hb + 4u * c : A.sk;
       __hip_atomic_fetch_add((lds_u32*)(size_t)a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
   }
+  const int below_tot = 0;
+  (void)below;
 #endif
-  const int below_tot = wave_sum((int)below);
   __builtin_amdgcn_wave_barrier();
   const uint2 hv = reinterpret_cast<const uint2*>(hist)[lane];
   const int sl = (int)(hv.x + hv.y);
@@ -461,6 +463,9 @@ __device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned 
   const int Es = __builtin_amdgcn_readlane(E, src);
   const int h0 = __builtin_amdgcn_readlane((int)hv.x, src), h1 = __builtin_amdgcn_readlane((int)hv.y, src);
   const bool second = r >= Es + h0;
+#ifndef ACOSS_HIST_MASKED
+  if (cmin && src == 0 && !second) return false;  // bin 0 of a window above 0: not an exact prefix
+#endif
   *P = base8 + 2u * (unsigned)src + (second ? 1u : 0u);
   *less = below_tot + Es + (second ? h0 : 0);
   *le = *less + (second ? h1 : h0);
@@ -514,6 +519,8 @@ struct Line {
     // tail; lanes past the line re-read lane 0's run and mask all of it. No per-element
     // conditional loads: hipcc branches around each and waits vmcnt(0) after each (16-32
     // serial L2 round trips per line)
+    // (lanes past the line reading a constant run of kNone instead of the fill below: -1 % at
+    // 2,000 frames, profiles/r04/ab_q2000.txt)
     const uint16_t* src = col0 + (base < n ? (size_t)lane * lane_stride : (size_t)0);
     win = false;
     base8 = 0u;
@@ -1682,18 +1689,12 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
 #else
   constexpr bool kPF = KQ != 2;
 #endif
-  LT Lnext;
-  if (kPF && i0 + w * RPW < V.Mp) load_row(Lnext, i0 + w * RPW);
-#pragma unroll 1
-  for (int r = w * RPW; r < (w + 1) * RPW; ++r) {
+  // one row's select on its loaded line L; prefetch() requests the wave's next line once this
+  // one's window is built
+  auto row = [&](LT& L, int r, auto&& prefetch) {
     const int i = i0 + r;
     uint64_t word = 0;  // (Line2: the second half's word in bits 32..63)
     if (i < V.Mp) {
-      LT L;
-      if constexpr (kPF)
-        L = Lnext;
-      else
-        load_row(L, i);
 #ifndef ACOSS_NO_WINDOW8
 #ifndef ACOSS_NO_SAMPLE_HINT
       if (hint.P == kNoHint) hint.P = sample_hint(L, V.Np, kappa);
@@ -1702,7 +1703,7 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
         if (hint.P != kNoHint) L.build_window(hint.P);
       }
 #endif
-      if (kPF && r + 1 < (w + 1) * RPW && i + 1 < V.Mp) load_row(Lnext, i + 1);
+      prefetch();
       const LineCells<true> keyf{V, i};
       float th, T;
       Group c_lo, c_hi;
@@ -1719,6 +1720,26 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
     }
     rowbits[r][lane] = (uint32_t)word;
     if constexpr (KQ == 2) rowbits[r][64 + lane] = (uint32_t)(word >> 32);
+  };
+  // (unrolled by two for long lines, each line in its own registers instead of the copy of the
+  // prefetched line: neutral, profiles/r04/ab_unroll2000.txt)
+  const int r1 = (w + 1) * RPW;
+  {
+    LT Lnext;
+    if (kPF && i0 + w * RPW < V.Mp) load_row(Lnext, i0 + w * RPW);
+#pragma unroll 1
+    for (int r = w * RPW; r < r1; ++r) {
+      LT L;
+      if (i0 + r < V.Mp) {
+        if constexpr (kPF)
+          L = Lnext;
+        else
+          load_row(L, i0 + r);
+      }
+      row(L, r, [&] {
+        if (kPF && r + 1 < r1 && i0 + r + 1 < V.Mp) load_row(Lnext, i0 + r + 1);
+      });
+    }
   }
   __syncthreads();
   // transpose: word of column j = bit (j & 31) of rowbits[r][j >> 5], r = 0..31. Thread b takes
@@ -1918,24 +1939,8 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
       Ld.load([&](int e) { return col + (unsigned)((e >> 5) * ldc * kSR + (e & 15) * 2 + ((e >> 4) & 1)); }, V.Mp);
     }
   };
-#ifdef ACOSS_COLS_NOPF  // no next-column prefetch: 16 VGPRs fewer (occupancy over latency)
-#pragma unroll 1
-  for (int j = j0; j < jend; ++j) {
-    LT L;
-    load_col(L, j);
-#else
-  constexpr bool kPF = KQ != 2;  // as the rows
-  LT Lnext;
-  if (kPF && j0 < jend) load_col(Lnext, j0);
-#pragma unroll 1
-  for (int j = j0; j < jend; ++j) {
-    LT L;
-    if constexpr (kPF)
-      L = Lnext;
-    else
-      load_col(L, j);
-    if (kPF && j + 1 < jend) load_col(Lnext, j + 1);
-#endif
+  // one column's select on its loaded line L
+  auto column = [&](LT& L, int j) {
 #ifndef ACOSS_NO_WINDOW8
 #ifndef ACOSS_NO_SAMPLE_HINT
     if (hint.P == kNoHint) hint.P = sample_hint(L, V.Mp, kappa);
@@ -1971,7 +1976,33 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
     if (KQ == 2 && 2048 + lane * KPL < V.Mp) maskT[w2] = (uint32_t)(bits >> 32) & rt2;
     ACOSS_STAMP(tc1);
     ACOSS_STAMP_ADD(35, tc0, tc1);  // le_bits and the CRP word
+  };
+#ifdef ACOSS_COLS_NOPF  // no next-column prefetch: 16 VGPRs fewer (occupancy over latency)
+#pragma unroll 1
+  for (int j = j0; j < jend; ++j) {
+    LT L;
+    load_col(L, j);
+    column(L, j);
   }
+#else
+  constexpr bool kPF = KQ != 2;  // as the rows
+  // (both columns of a long-line pair in their own registers, fully unrolled, instead of the
+  // copy of the prefetched line: -4.5 % at 2,000 frames, profiles/r04/ab_unroll2000.txt)
+  {
+    LT Lnext;
+    if (kPF && j0 < jend) load_col(Lnext, j0);
+#pragma unroll 1
+    for (int j = j0; j < jend; ++j) {
+      LT L;
+      if constexpr (kPF)
+        L = Lnext;
+      else
+        load_col(L, j);
+      if (kPF && j + 1 < jend) load_col(Lnext, j + 1);
+      column(L, j);
+    }
+  }
+#endif
 }
 
 
