@@ -336,9 +336,69 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w(const float* __r
 // takes 16 rows (one wave per row) and writes them as one row of u16 bit words (bit r = row
 // 16g + r) in LDS, then to the pair's bit plane for SW. blockIdx.z = CSM plane, written to
 // bit plane z + plane0 of the pair (plane stride = wplane words, 4 planes per pair).
+// The nn-th smallest (1-based) of the wave's keys kr (KB per lane) within [lo, hi], by radix
+// select: from the highest bit where lo and hi differ, 8-bit digits, each digit from one LDS
+// histogram of the candidates (keys matching the digits so far) and one wave scan of its 256
+// bins; about 4 passes instead of the ~26 count passes of a bisection over [lo, hi]. Every key
+// issues one unconditional ds_add: candidates to their digit's bin, the rest to a lane-private
+// sink word (hist: 256 bins + 64 sink words, this wave's own). Same answer as the bisection:
+// the least key v with #(keys <= v) >= nn.
+template <int KB>
+__device__ __forceinline__ unsigned radix_kth(const unsigned (&kr)[KB], unsigned lo, unsigned hi, int nn, int lane,
+                                              unsigned* hist) {
+  if (lo >= hi) return lo;
+  typedef __attribute__((address_space(3))) unsigned lds_u32;
+  const unsigned hb = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(size_t)(lds_u32*)hist);
+  const unsigned sk = hb + 1024u + 4u * (unsigned)lane;
+  int sh = 32 - __builtin_clz(lo ^ hi);  // bits [0, sh) differ inside [lo, hi]
+  unsigned prefix = sh >= 32 ? 0u : (lo >> sh) << sh;
+  int rank = nn - 1;
+  while (sh > 0) {  // wave-uniform
+    const int dsh = sh > 8 ? sh - 8 : 0;
+    reinterpret_cast<uint4*>(hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    const unsigned P = sh >= 32 ? 0u : prefix >> sh;
+#pragma unroll
+    for (int q = 0; q < KB; ++q) {
+      const unsigned k = kr[q];
+      const bool cand = sh >= 32 || (k >> sh) == P;
+      const unsigned d = (k >> dsh) & 0xffu;
+      const unsigned a = cand ? hb + 4u * d : sk;
+      __hip_atomic_fetch_add((lds_u32*)(size_t)a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint4 hv = reinterpret_cast<const uint4*>(hist)[lane];  // bins 4 lane .. 4 lane + 3
+    const int sl = (int)(hv.x + hv.y + hv.z + hv.w);
+    const int S = wave_incl_scan(sl);
+    const int E = S - sl;
+    const int src = __builtin_ctzll(__ballot(E <= rank && rank < S));
+    int r = rank - __builtin_amdgcn_readlane(E, src);
+    const int h0 = __builtin_amdgcn_readlane((int)hv.x, src), h1 = __builtin_amdgcn_readlane((int)hv.y, src),
+              h2 = __builtin_amdgcn_readlane((int)hv.z, src);
+    unsigned b = 0;
+    if (r >= h0) {
+      r -= h0;
+      b = 1;
+      if (r >= h1) {
+        r -= h1;
+        b = 2;
+        if (r >= h2) {
+          r -= h2;
+          b = 3;
+        }
+      }
+    }
+    prefix |= (4u * (unsigned)src + b) << dsh;
+    rank = r;
+    sh = dsh;
+    __builtin_amdgcn_wave_barrier();
+  }
+  return prefix;
+}
+
 template <int KB>  // keys per lane held in registers (rows of up to 64 * KB columns)
 __device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int N, double kappa, int lane,
-                                                unsigned* bits, unsigned bit) {
+                                                unsigned* bits, unsigned bit, unsigned* hist) {
   if (kappa == 0.0) {
     for (int c = lane; c < N; c += 64) atomicOr(&bits[c], bit);
     return;
@@ -361,6 +421,7 @@ __device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int
     }
     lo = wave_min_u32(mn);
     hi = wave_max_u32(mx);
+#ifdef ACOSS_EF_BISECT  // (the count-pass bisection, for A/B)
     while (lo < hi) {
       const unsigned mid = lo + ((hi - lo) >> 1);
       int c = 0;
@@ -371,6 +432,9 @@ __device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int
       else
         lo = mid + 1;
     }
+#else
+    lo = radix_kth(kr, lo, hi, nn, lane, hist);
+#endif
   } else {
     while (lo < hi) {
       const unsigned mid = lo + ((hi - lo) >> 1);
@@ -425,6 +489,7 @@ __global__ __launch_bounds__(1024) void k_ef_binarize(const float* __restrict__ 
                                                       EfPairs E, double kappa, uint16_t* __restrict__ Wb,
                                                       int64_t wplane, int plane0) {
   extern __shared__ unsigned bits[];
+  __shared__ __attribute__((aligned(16))) unsigned s_hist[16][256 + 64];  // radix_kth, one per wave
   const int p = blockIdx.y, m = blockIdx.z, g = blockIdx.x;
   int a, b, M, N;
   pair_dims(E, p, &a, &b, &M, &N);
@@ -436,9 +501,9 @@ __global__ __launch_bounds__(1024) void k_ef_binarize(const float* __restrict__ 
   if (row < M) {
     const float* xr = C + m * mat_stride + (size_t)p * ld * ld + (size_t)row * ld;
     if (N <= 64 * 8)  // EarlyFusion's ~450-block tracks: 8 key registers halve the count passes
-      ef_binarize_row<8>(xr, N, kappa, lane, bits, 1u << w);
+      ef_binarize_row<8>(xr, N, kappa, lane, bits, 1u << w, s_hist[w]);
     else
-      ef_binarize_row<kBinRegs>(xr, N, kappa, lane, bits, 1u << w);
+      ef_binarize_row<kBinRegs>(xr, N, kappa, lane, bits, 1u << w, s_hist[w]);
   }
   __syncthreads();
   uint16_t* o = Wb + ((size_t)p * 4 + plane0 + m) * wplane + (size_t)g * ld;
