@@ -259,7 +259,11 @@ def other_paths(nth, seed):
                                            "per_thread": round(ncpu / cdt / nth, 3),
                                            "sample": "%d pairs, numpy restatement + C SW oracle on %d threads "
                                                      "(BLAS 1 thread each), %.1f s" % (ncpu, nth, cdt)},
-                          "scores_equal_to_oracle": "%d of %d" % (agree, 4 * ncpu)}
+                          "scores_equal_to_oracle": "%d of %d" % (agree, 4 * ncpu),
+                          "scores_note": "the restatement's CSMs here are numpy/BLAS products (another float "
+                                         "summation order than the GPU's fmaf chain), so a kNN tie can flip on "
+                                         "random features; on integer-exact block features the GPU scores equal the "
+                                         "oracle composition bit for bit (tests/test_gpu_earlyfusion_pin.py)"}
     # ---- SNF cross-diffusion step (f2) at Da-TACOS size
     res["snf"] = snf_path(seed)
     return res
