@@ -382,10 +382,12 @@ __device__ __forceinline__ uint32_t gather_flags8(uint32_t acc, uint32_t s, int 
   return ((s >> (7 - h)) & (0x01010101u << h)) | acc;
 }
 
-// One element into the LDS prefix histogram: bin c when `in`, else this lane's own sink word (the
-// 64 words after the 128 bins, WaveLds::sink), so that every element issues the same
-// unconditional ds_add (a lane-private address: no bank conflict) instead of a compare, an exec
-// mask save / restore and a masked add per element (ACOSS_HIST_MASKED: the masked form, for A/B).
+// Unconditional histogram adds: an element outside the bins goes to this lane's own sink word
+// (the 64 words after the 128 bins, WaveLds::sink; a lane-private address, no bank conflict), so
+// every element issues the same ds_add instead of a compare, an exec-mask save / restore and a
+// masked add. Used by the window-code histogram (hist_rank_w8; ACOSS_HIST_MASKED restores the
+// masked form there, for A/B); the 16-bit-prefix histograms keep the masked add (hist_add below),
+// where the sink measured 6 % slower at 500 frames (ACOSS_HIST_SINK_PV, for A/B).
 typedef __attribute__((address_space(3))) unsigned lds_u32;
 // 32-bit LDS addresses of a wave's histogram: the bins' base as an SGPR (bin address = c * 4 +
 // base in one v_lshl_add) and this lane's sink word
