@@ -1,7 +1,10 @@
 """One rank of tests/test_gpu_multirank.py (not a test module): runs a plugin's real HIP
 all_pairwise under torch.distributed (gloo; the ranks share one GPU) and rank 0 saves Ds.
 Usage: python tests/multirank_worker.py ALGO CSV FEATURE_DIR CACHEDIR OUT.npz
-(RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT from the environment)."""
+(RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT from the environment). ACOSS_MR_DOWNSAMPLE: Serra09's
+downsample_fac (default: the reference's); ACOSS_MR_SIMPLE_WIN / _SKIP: SiMPle's WIN / SKIP on
+crema (default: the reference's hpcp, 200 / 100); ACOSS_MR_DIGEST=1: save a SHA-256 of every Ds matrix
+(and its shape) instead of the matrix (the 15,000-song runs)."""
 import os
 import sys
 
@@ -25,7 +28,10 @@ def main():
     os.chdir(cachedir)
     if algo == "Serra09":
         from acoss.algorithms.rqa_serra09 import Serra09
-        a = Serra09(csv, fdir, shortname="mr", cachedir=cachedir)
+        kw = {}
+        if os.environ.get("ACOSS_MR_DOWNSAMPLE"):
+            kw["downsample_fac"] = int(os.environ["ACOSS_MR_DOWNSAMPLE"])
+        a = Serra09(csv, fdir, shortname="mr", cachedir=cachedir, **kw)
         a.all_pairwise(symmetric=True)
         a.normalize_by_length()
     elif algo in ("ChenFusion", "ChenLate"):
@@ -47,10 +53,23 @@ def main():
         a.do_late_fusion()
     else:
         from acoss.algorithms.simple_silva import Simple
-        a = Simple(csv, fdir, shortname="mr", cachedir=cachedir)
+        kw = {}
+        if os.environ.get("ACOSS_MR_SIMPLE_WIN"):  # (window / hop of the SiMPle features)
+            kw = {"chroma_type": "crema", "WIN": int(os.environ["ACOSS_MR_SIMPLE_WIN"]),
+                  "SKIP": int(os.environ["ACOSS_MR_SIMPLE_SKIP"])}
+        a = Simple(csv, fdir, shortname="mr", cachedir=cachedir, **kw)
         a.all_pairwise(symmetric=False)
     if rank == 0:
-        np.savez(out, **{k: np.asarray(v) for k, v in a.Ds.items()})
+        if os.environ.get("ACOSS_MR_DIGEST") == "1":
+            import hashlib
+            dig = {}
+            for k, v in a.Ds.items():
+                arr = np.ascontiguousarray(np.asarray(v))
+                dig[k] = np.array([hashlib.sha256(arr.tobytes()).hexdigest(), str(arr.shape),
+                                   str(int(np.isfinite(arr).sum()))])
+            np.savez(out, **dig)
+        else:
+            np.savez(out, **{k: np.asarray(v) for k, v in a.Ds.items()})
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -43,7 +43,7 @@ def datacos_mini(tmp_path_factory):
     return root, csv, fdir
 
 
-def _run(algo, world, root, csv, fdir, tag, env_extra=None):
+def _run(algo, world, root, csv, fdir, tag, env_extra=None, timeout=240):
     out = str(root / ("%s_%s_w%d.npz" % (algo, tag, world)))
     cache = str(root / ("cache_%s_%s_w%d" % (algo, tag, world)))
     port = _free_port()
@@ -56,7 +56,7 @@ def _run(algo, world, root, csv, fdir, tag, env_extra=None):
     logs = []
     for p in procs:
         try:
-            o, _ = p.communicate(timeout=240)
+            o, _ = p.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
