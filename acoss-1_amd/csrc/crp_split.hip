@@ -300,7 +300,42 @@ __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int str
         }
       }
     }
-#ifdef ACOSS_ABL_NOHC  // timing ablation only (wrong results): no strip-major plane stores
+#ifndef ACOSS_HC_LANE_STORES
+    // strip-major stores in 64-byte runs: a 4 x 4 transpose of the 16-byte pieces inside each lane
+    // quad (two DPP butterfly stages per piece word), then store k: lane b + m (b = lane & ~3)
+    // writes piece m of lane b + k's column, so a quad writes one column's 64 bytes contiguously
+    // (each lane writing its own column's four pieces at a 64-byte stride: ACOSS_HC_LANE_STORES,
+    // 1.5 % slower at 2,000 frames, profiles/r04/ab_hcquad2000.txt)
+    {
+      const int m = lane & 3, b = lane & ~3;
+      const bool o1 = (m & 1) != 0, o2 = (m & 2) != 0;
+      uint32_t T[4][4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t x0 = hw[d], x1 = hw[4 + d], x2 = hw[8 + d], x3 = hw[12 + d];
+        // every DPP on all lanes (left to itself the compiler sinks them under the selects' exec
+        // masks, where the partner lane is off and reads as 0)
+        uint32_t p0 = dpp_u32<0xB1>(x0, x0), p1 = dpp_u32<0xB1>(x1, x1), p2 = dpp_u32<0xB1>(x2, x2),
+                 p3 = dpp_u32<0xB1>(x3, x3);
+        asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3));
+        const uint32_t y0 = o1 ? p1 : x0, y1 = o1 ? x1 : p0, y2 = o1 ? p3 : x2, y3 = o1 ? x3 : p2;
+        uint32_t q0 = dpp_u32<0x4E>(y0, y0), q1 = dpp_u32<0x4E>(y1, y1), q2 = dpp_u32<0x4E>(y2, y2),
+                 q3 = dpp_u32<0x4E>(y3, y3);
+        asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
+        T[0][d] = o2 ? q2 : y0;
+        T[1][d] = o2 ? q3 : y1;
+        T[2][d] = o2 ? y2 : q0;
+        T[3][d] = o2 ? y3 : q1;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = jb + b + k - (kMS - 1);
+        if (b + k >= kMS - 1 && c < V.Np)
+          reinterpret_cast<uint4*>(Hc + ((size_t)strip * ldc + c) * kSR)[m] = make_uint4(T[k][0], T[k][1], T[k][2], T[k][3]);
+      }
+    }
+    if (false) {
+#elif defined(ACOSS_ABL_NOHC)  // timing ablation only (wrong results): no strip-major plane stores
     if (hw[0] == 0x12345678u && hw[15] == 0x9abcdef0u) {
 #else
     if (valid) {
