@@ -99,10 +99,16 @@ def _check(rc, what):
         raise AcossHipError("%s failed (%s): %s" % (what, _ERRNAMES.get(rc, rc), msg))
 
 
+_BOUND = [False]
+
+
 def _torch():
     import torch
     if not torch.cuda.is_available():
         raise AcossHipError("no HIP GPU visible to torch: the acoss HIP engine has no CPU fallback")
+    if not _BOUND[0]:  # one process per GPU under RCCL: bind before the first "cuda" allocation
+        from .distributed import bind_local_device
+        _BOUND[0] = bind_local_device() is not None
     return torch
 
 
@@ -488,6 +494,38 @@ def simple_features(feats, track_off, track_len, win=200, skip=100, win_len_smoo
     return out[:total], out_off, T.astype(np.int32)
 
 
+def ef_neighbour_error(nb_query, nb_ref, kappa, K):
+    """The ValueError the reference raises for a pair of block counts, or None (host-only, no GPU).
+    csm_to_binary takes argpartition(D, nn, 1) with nn = round(kappa * ncols) (kappa < 1) or kappa,
+    which raises unless nn < ncols (cross_recurrence.py:150-156); getWCSM takes np.partition(CSM, K)
+    along the columns and the rows, which raises unless K < ncols and K < nrows
+    (similarity_fusion.py:47-50). nb_query / nb_ref: block counts (arrays) of each pair's songs."""
+    nq = np.asarray(nb_query, np.int64)
+    nr = np.asarray(nb_ref, np.int64)
+    if kappa != 0:
+        nn = np.round(kappa * nr).astype(np.int64) if kappa < 1 else np.full(nr.shape, int(kappa), np.int64)
+        bad = np.flatnonzero(nn >= nr)
+        if len(bad):
+            b = bad[0]
+            return ValueError("kth(=%d) out of bounds (%d)" % (nn[b], nr[b]))
+    bad = np.flatnonzero((K >= nr) | (K >= nq))
+    if len(bad):
+        b = bad[0]
+        return ValueError("kth(=%d) out of bounds (%d)" % (K, min(nr[b], nq[b])))
+    return None
+
+
+def _check_ef_neighbours(bank, pairs, kappa, K):
+    """Reject pairs whose block counts the reference's argpartition / partition would refuse (see
+    ef_neighbour_error) before the kernels run. The smallest counts decide: both conditions are
+    monotone in the block count (n - round(kappa n) never decreases with n for kappa < 1)."""
+    nbp = bank["nb"].long()[pairs.long()]
+    lo_q, lo_r = int(nbp[:, 0].min()), int(nbp[:, 1].min())
+    err = ef_neighbour_error([lo_q], [lo_r], kappa, K)
+    if err is not None:
+        raise err
+
+
 def earlyfusion(bank, pairs, kappa=0.1, K=10, mu=0.5):
     """Batched EarlyFusion scores (earlyfusion_traile.py:157-198). bank: dict of device tensors
     'mfccs', 'ssms', 'chromas' (sum nb x d, float32), 'chroma_med' (T x 12), 'off' (T,) int64,
@@ -501,6 +539,7 @@ def earlyfusion(bank, pairs, kappa=0.1, K=10, mu=0.5):
     out = torch.empty((P, 4), dtype=torch.float64, device="cuda")
     if P == 0:
         return out
+    _check_ef_neighbours(bank, pairs, kappa, K)
     rc = lib.acoss_earlyfusion(_ptr(bank["mfccs"]), _ptr(bank["ssms"]), _ptr(bank["chromas"]), _ptr(bank["chroma_med"]),
                                _ptr(bank["off"]), _ptr(bank["nb"]), int(bank["nb"].shape[0]), int(bank["max_blocks"]),
                                int(bank["mfccs"].shape[1]), int(bank["ssms"].shape[1]), int(bank["chromas"].shape[1]),

@@ -11,15 +11,21 @@ What changes is how the pair loop runs (algorithm_template.py:142-193). The refe
     reference does) and lets the subclass build its device-resident banks;
   * the pairs, in the reference's enumeration order (combinations / permutations), go to
     `similarity` in large chunks; the subclasses score a chunk with one batched HIP call;
-  * with torch.distributed initialised (one process per GPU, RCCL), every rank scores one
-    cost-balanced row stripe (acoss.distributed) and ONE all-gather assembles Ds on every
-    rank; `parallel` / `n_cores` are accepted for signature compatibility and ignored;
+  * with torch.distributed initialised (one process per GPU, RCCL), every rank is bound to its
+    local rank's GPU (acoss.distributed.bind_local_device), scores one cost-balanced row stripe
+    and ONE exchange assembles Ds: a gather onto rank 0 for the scorers that rank 0 alone
+    finishes (Serra09, SiMPle), an all-gather onto every rank for those whose SNF late fusion
+    runs on every rank next (`_Ds_on_every_rank`: ChenFusion, EarlyFusion); `parallel` /
+    `n_cores` are accepted for signature compatibility and ignored;
   * subclasses with a HIP scorer (`_device_scores`) keep the stripe on the device: the
     all-gather, `Ds += Ds.T` and the subclasses' normalize_by_length run as HIP kernels
     (finish.hip), and getEvalStatistics ranks on the device (acoss_eval_ranks), so no O(N^2)
     host loop is left for Da-TACOS-sized runs (SURVEY.md §8f row 1);
   * every rank keeps Ds in a file-backed memmap of its own (rank 0: the reference's file, other
-    ranks '<file>.rank<r>'), and only rank 0 writes the results, so ranks never write one file;
+    ranks '<file>.rank<r>', unlinked as soon as it is mapped, so it never outlives the process),
+    and only rank 0 prints the statistics and writes the results CSV and the Ds file, so ranks
+    never write one file (the reference's single shared memmap and results file, :172-177,
+    :277-290); ranks that do not hold Ds get rank 0's statistics from getEvalStatistics;
   * Ds is saved as '<prefix>_Ds.h5' (the reference's file, :163,193; one dataset per
     similarity type, as deepdish lays out a dict) when h5py is importable, and always as the
     '<prefix>_Ds.npz' twin; `precomputed=True` reads either back.
@@ -72,9 +78,29 @@ class CoverAlgorithm(object):
         self.Ds = {}
         _, rank = _dist_info()
         for s in similarity_types:
-            self.Ds[s] = np.memmap(self._dmat_path(s, rank), shape=(self.N, self.N), mode="w+", dtype="float32")
+            self.Ds[s] = self._new_dmat(s, rank)
         self._prepared = False
-        print("Initialized %s algorithm on %i songs in dataset %s" % (name, self.N, shortname))
+        self._holds_Ds = True         # this rank's Ds hold the assembled matrices
+        self._stats_from_root = False  # getEvalStatistics takes rank 0's statistics (world > 1)
+        if rank == 0:
+            print("Initialized %s algorithm on %i songs in dataset %s" % (name, self.N, shortname))
+
+    # Ds assembled on every rank (all-gather) instead of rank 0 only (gather): subclasses whose
+    # late fusion runs on every rank after all_pairwise (ChenFusion, EarlyFusion) set this
+    _Ds_on_every_rank = False
+
+    def _new_dmat(self, s, rank):
+        """Ds[s] as a float32 (N, N) memmap (:61). Rank r > 0's file is unlinked once mapped: the
+        mapping stays valid (POSIX), the disk blocks are freed when the process ends, and nothing
+        is left in cachedir (0.9 GB per matrix and rank at Da-TACOS size)."""
+        path = self._dmat_path(s, rank)
+        mm = np.memmap(path, shape=(self.N, self.N), mode="w+", dtype="float32")
+        if rank != 0:
+            try:
+                os.remove(path)
+            except OSError:
+                pass
+        return mm
 
     # ------------------------------------------------------------------ features
     def get_cacheprefix(self):
@@ -152,20 +178,26 @@ class CoverAlgorithm(object):
         if precomputed:
             self._load_Ds(prefix)
             self.get_all_clique_ids()
+            self._holds_Ds, self._stats_from_root = True, False
             return
-        self.prepare()
         world, rank = _dist_info()
+        if world > 1:
+            _dist.bind_local_device()
+        self.prepare()
         if world > 1:
             bounds = _dist.stripe_bounds(self.track_lengths(), world, symmetric, m=0, tau=0)
         else:
             bounds = [(0, self.N)]
         r0, r1 = bounds[rank]
-        if not self._device_all_pairwise(bounds, r0, r1, world, symmetric):
+        every = world == 1 or self._Ds_on_every_rank
+        self._holds_Ds = every or rank == 0
+        self._stats_from_root = not every
+        if not self._device_all_pairwise(bounds, r0, r1, world, symmetric, every):
             for chunk in self._pair_chunks(r0, r1, symmetric):
                 self.similarity(chunk)
             if world > 1:
-                self._gather_stripes(bounds, r0, r1)
-            if symmetric:
+                self._gather_stripes(bounds, r0, r1, every)
+            if symmetric and self._holds_Ds:
                 for key in self.Ds:
                     self.Ds[key] += self.Ds[key].T
         if rank == 0:
@@ -188,10 +220,11 @@ class CoverAlgorithm(object):
                 last = now
                 print("%s: %d / %d pairs, %.1f s" % (self.name, done, n_pairs, now - t0), file=sys.stderr, flush=True)
 
-    def _device_all_pairwise(self, bounds, r0, r1, world, symmetric):
+    def _device_all_pairwise(self, bounds, r0, r1, world, symmetric, every=True):
         """The pair loop with the stripe kept in HBM: score chunks on the device, scatter into
-        the (r1 - r0, N) stripe, one all-gather (world > 1), symmetrise with acoss_ds_finish,
-        one copy into Ds. Returns False if the subclass has no device scorer."""
+        the (r1 - r0, N) stripe, one exchange (world > 1: all-gather if `every`, else a gather onto
+        rank 0), symmetrise with acoss_ds_finish and copy into Ds on the ranks that receive the
+        matrix. Returns False if the subclass has no device scorer."""
         if type(self)._device_scores is CoverAlgorithm._device_scores:
             return False
         import torch
@@ -204,21 +237,29 @@ class CoverAlgorithm(object):
                 blocks[k][p[:, 0] - r0, p[:, 1]] = sc[k]
         for k in list(blocks):
             blk = blocks.pop(k)
-            full = _dist.all_gather_stripes(blk, bounds) if world > 1 else blk
+            if world == 1:
+                full = blk
+            elif every:
+                full = _dist.all_gather_stripes(blk, bounds)
+            else:
+                full = _dist.gather_stripes(blk, bounds, dst=0)
             del blk
+            if full is None:  # not the root of the gather
+                continue
             if symmetric:
                 _lib.ds_finish(full, symmetric=True)
             self.Ds[k][:] = full.cpu().numpy()
             del full  # one assembled matrix on the device at a time
         return True
 
-    def _gather_stripes(self, bounds, r0, r1):
+    def _gather_stripes(self, bounds, r0, r1, every=True):
         import torch
         dev = "cuda" if torch.cuda.is_available() else "cpu"
         for key in self.Ds:
             blk = torch.as_tensor(np.array(self.Ds[key][r0:r1])).to(dev)
-            full = _dist.all_gather_stripes(blk, bounds)
-            self.Ds[key][:] = full.cpu().numpy()
+            full = _dist.all_gather_stripes(blk, bounds) if every else _dist.gather_stripes(blk, bounds, dst=0)
+            if full is not None:
+                self.Ds[key][:] = full.cpu().numpy()
 
     def _finish_device(self, norm, mode):
         """normalize_by_length on the device for every Ds key (acoss_ds_finish, mode 'serra09' or
@@ -271,21 +312,35 @@ class CoverAlgorithm(object):
     # ------------------------------------------------------------------ evaluation
     def getEvalStatistics(self, similarity_type, topsidx=[1, 10, 100, 1000]):
         """MR, MRR, MDR, MAP, Top-k of Ds[similarity_type] (:206-291); prints them and appends
-        a row to 'results_<shortname>_<name>.csv'."""
+        a row to 'results_<shortname>_<name>.csv'. Under torch.distributed only rank 0 prints and
+        writes the row (one row per call, as the reference's single process writes). When Ds was
+        gathered onto rank 0 only, rank 0 computes the statistics and broadcasts them, so every rank
+        must call this (coverid.benchmark does) and every rank returns the same values."""
+        world, rank = _dist_info()
+        stats = None
+        if self._holds_Ds and (rank == 0 or not self._stats_from_root):
+            stats = self._eval_stats(similarity_type, topsidx)
+        if world > 1 and self._stats_from_root:
+            import torch.distributed as dist
+            box = [stats]
+            dist.broadcast_object_list(box, src=0)
+            stats = box[0]
+        MR, MRR, MDR, MAP, tops = stats
+        if rank == 0:
+            if np.isnan(MR):
+                warnings.warn("no clique with at least two songs")
+            print("%s %s STATS\n-------------------------\nMR = %.3g\nMRR = %.3g\nMDR = %.3g\nMAP = %.3g"
+                  % (self.name, similarity_type, MR, MRR, MDR, MAP))
+            for t, v in zip(topsidx, tops):
+                print("Top-%i: %i" % (t, v))
+            evaluation.write_results_csv("results_%s_%s.csv" % (self.shortname, self.name), self.name,
+                                         similarity_type, stats, topsidx)
+        return MR, MRR, MDR, MAP, tops
+
+    def _eval_stats(self, similarity_type, topsidx):
         D = np.array(self.Ds[similarity_type], dtype=np.float32)
         cliques = [sorted(self.cliques[s]) for s in self.cliques]
         if _on_gpu():  # the O(N^2) rank step as a HIP kernel (same statistics, same host code)
             import torch
-            stats = evaluation.eval_statistics_device(torch.as_tensor(D).cuda(), cliques=cliques, topsidx=topsidx)
-        else:  # the reference's own host computation, restated (no GPU in this process)
-            stats = evaluation.eval_statistics_cliques(D, cliques, topsidx)
-        MR, MRR, MDR, MAP, tops = stats
-        if np.isnan(MR):
-            warnings.warn("no clique with at least two songs")
-        print("%s %s STATS\n-------------------------\nMR = %.3g\nMRR = %.3g\nMDR = %.3g\nMAP = %.3g"
-              % (self.name, similarity_type, MR, MRR, MDR, MAP))
-        for t, v in zip(topsidx, tops):
-            print("Top-%i: %i" % (t, v))
-        evaluation.write_results_csv("results_%s_%s.csv" % (self.shortname, self.name), self.name, similarity_type,
-                                     stats, topsidx)
-        return MR, MRR, MDR, MAP, tops
+            return evaluation.eval_statistics_device(torch.as_tensor(D).cuda(), cliques=cliques, topsidx=topsidx)
+        return evaluation.eval_statistics_cliques(D, cliques, topsidx)  # the reference's host computation

@@ -52,6 +52,9 @@ def resize_block(X, i1, i2, frames_per_block, median_aggregate=False):
 
 
 class EarlyFusion(CoverAlgorithm):
+    # the SNF late fusion runs on every rank (row-sharded): every rank needs the assembled Ds
+    _Ds_on_every_rank = True
+
     def __init__(self, dataset_csv, datapath, chroma_type='hpcp', shortname='Covers80', blocksize=20,
                  mfccs_per_block=50, ssm_res=50, chromas_per_block=40, kappa=0.1, K=10, niters=5, log_times=False,
                  cachedir="cache"):

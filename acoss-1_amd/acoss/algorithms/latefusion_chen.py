@@ -19,6 +19,9 @@ __all__ = ["ChenFusion"]
 
 
 class ChenFusion(ChromaBackedAlgorithm):
+    # the SNF late fusion runs on every rank (row-sharded): every rank needs the assembled Ds
+    _Ds_on_every_rank = True
+
     def __init__(self, dataset_csv, datapath, chroma_type='hpcp', shortname='benchmark', oti=True, kappa=0.095,
                  tau=1, m=9, downsample_fac=40, cachedir="cache"):
         self._init_chroma(chroma_type, oti, kappa, tau, m, downsample_fac)

@@ -3,11 +3,53 @@
 One process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on ROCm, "gloo" on
 CPU for tests). The pair matrix is split into contiguous ROW STRIPES whose cost
 sum_i sum_j M'_i N'_j is balanced; every rank scores only its stripe (no data-path
-collective), then ONE all-gather of the stripes assembles the full score matrix on every
-rank — the exchange step that replaces the reference's shared np.memmap
-(acoss/algorithms/algorithm_template.py:61,174-177).
+collective), then ONE exchange assembles the full score matrix — the step that replaces the
+reference's shared np.memmap (acoss/algorithms/algorithm_template.py:61,174-177): an all-gather
+onto every rank where every rank needs the matrices next (SNF late fusion, row-sharded), a gather
+onto rank 0 where only rank 0 finishes, evaluates and saves them.
 """
+import os
+
 import numpy as np
+
+# environment variables that name a process's rank on its node, in the order they are trusted
+# (torch.distributed.run / torchrun, Open MPI, MPICH / Intel MPI, Slurm)
+LOCAL_RANK_VARS = ("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "SLURM_LOCALID")
+
+
+def local_rank(rank, n_dev):
+    """This process's rank on its node: the launcher's variable, else rank % n_dev."""
+    for v in LOCAL_RANK_VARS:
+        s = os.environ.get(v)
+        if s is not None and s.strip().lstrip("-").isdigit():
+            return int(s)
+    return rank % max(1, n_dev)
+
+
+def bind_local_device():
+    """One process per GPU: under the nccl (RCCL) backend bind this rank to GPU
+    local_rank % device_count before the package allocates anything on "cuda".
+
+    Without it every rank of `torchrun --nproc-per-node 8` that never called
+    torch.cuda.set_device would allocate on cuda:0, and RCCL refuses (or serialises) several
+    ranks on one GPU. The rule: a process whose current device is the default (cuda:0) is moved
+    to its local rank's GPU; a process that already sits on its local rank's GPU, or that the
+    caller bound to another non-default GPU on purpose, is left where it is. Under gloo (CPU
+    collectives; ranks may share a GPU, as the tests do) nothing is bound. Returns the device
+    index this rank uses under nccl, else None."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_backend() != "nccl":
+        return None
+    if not torch.cuda.is_available():
+        return None
+    n = torch.cuda.device_count()
+    want = local_rank(dist.get_rank(), n) % n
+    cur = torch.cuda.current_device()
+    if cur != want and cur == 0:
+        torch.cuda.set_device(want)
+        cur = want
+    return cur
 
 
 def pair_cost(lens, i, j, m=9, tau=1):
@@ -98,5 +140,27 @@ def all_gather_stripes(blk, bounds, group=None):
     pad[: src.shape[0]] = src
     outs = [torch.empty_like(pad) for _ in bounds]
     dist.all_gather(outs, pad, group=group)
+    full = torch.cat([o[: r1 - r0] for o, (r0, r1) in zip(outs, bounds)], 0)
+    return full.to(blk.device) if host else full
+
+
+def gather_stripes(blk, bounds, dst=0, group=None):
+    """Assemble the full (n, n) matrix on rank `dst` only (one gather); other ranks get None.
+    For scorers whose matrices only the root finishes, evaluates and saves (Serra09, SiMPle): no
+    other rank receives, copies to host or writes the N x N matrix (0.9 GB per matrix at
+    Da-TACOS size)."""
+    import torch
+    import torch.distributed as dist
+    n = blk.shape[1]
+    rmax = max(r1 - r0 for r0, r1 in bounds)
+    host = dist.get_backend(group) == "gloo" and blk.is_cuda
+    src = blk.cpu() if host else blk
+    pad = torch.zeros((rmax, n), dtype=src.dtype, device=src.device)
+    pad[: src.shape[0]] = src
+    me = dist.get_rank(group)
+    outs = [torch.empty_like(pad) for _ in bounds] if me == dst else None
+    dist.gather(pad, gather_list=outs, dst=dst, group=group)
+    if me != dst:
+        return None
     full = torch.cat([o[: r1 - r0] for o, (r0, r1) in zip(outs, bounds)], 0)
     return full.to(blk.device) if host else full

@@ -403,7 +403,9 @@ __device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int
     for (int c = lane; c < N; c += 64) atomicOr(&bits[c], bit);
     return;
   }
-  const int nn = kappa < 1.0 ? (int)rint(kappa * (double)N) : (int)kappa;  // np.round: half to even
+  // np.round: half to even. The host wrapper rejects nn >= N as the reference's argpartition does;
+  // the clamp keeps the radix select's rank inside the row if the ABI is called directly
+  const int nn = min(kappa < 1.0 ? (int)rint(kappa * (double)N) : (int)kappa, N);
   if (nn <= 0) return;
   const int per = (N + 63) / 64;
   const int c0 = lane * per, c1 = min(N, c0 + per);

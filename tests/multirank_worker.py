@@ -1,7 +1,8 @@
 """One rank of tests/test_gpu_multirank.py (not a test module): runs a plugin's real HIP
 all_pairwise under torch.distributed (gloo; the ranks share one GPU) and rank 0 saves Ds.
 Usage: python tests/multirank_worker.py ALGO CSV FEATURE_DIR CACHEDIR OUT.npz
-(RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT from the environment). ACOSS_MR_DOWNSAMPLE: Serra09's
+(RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT from the environment). ALGO "bench:<name>" runs
+coverid.benchmark(algorithm=<name>) instead of the plugin calls. ACOSS_MR_DOWNSAMPLE: Serra09's
 downsample_fac (default: the reference's); ACOSS_MR_SIMPLE_WIN / _SKIP: SiMPle's WIN / SKIP on
 crema (default: the reference's hpcp, 200 / 100); ACOSS_MR_DIGEST=1: save a SHA-256 of every Ds matrix
 (and its shape) instead of the matrix (the 15,000-song runs)."""
@@ -26,7 +27,13 @@ def main():
         dist.init_process_group("gloo")
     os.makedirs(cachedir, exist_ok=True)
     os.chdir(cachedir)
-    if algo == "Serra09":
+    if algo.startswith("bench:"):
+        # the whole reference entry point (coverid.py:22-148): all_pairwise, normalisation, late
+        # fusion, getEvalStatistics on every key (only rank 0 writes results_mr_<name>.csv, in the
+        # cachedir: this process's cwd), cleanup_memmap
+        from acoss import coverid
+        a = coverid.benchmark(csv, fdir, algorithm=algo.split(":", 1)[1], shortname="mr", cachedir=cachedir)
+    elif algo == "Serra09":
         from acoss.algorithms.rqa_serra09 import Serra09
         kw = {}
         if os.environ.get("ACOSS_MR_DOWNSAMPLE"):

@@ -89,3 +89,30 @@ def test_oracle_block_features_match_reference_loop():
     # the product's public resize_block and the oracle's are the same restatement
     from acoss.algorithms.earlyfusion_traile import resize_block
     np.testing.assert_array_equal(resize_block(mfcc, 5, 300, 50), npo.resize_block(mfcc, 5, 300, 50))
+
+
+def _reference_raises(nq, nr, kappa, K):
+    """Run the reference's own partition calls of one EarlyFusion pair (csm_to_binary,
+    cross_recurrence.py:150-156, then getWCSM, similarity_fusion.py:47-50) on a (nq, nr) CSM."""
+    D = np.arange(nq * nr, dtype=np.float32).reshape(nq, nr)
+    try:
+        if kappa != 0:
+            np.argpartition(D, npo.nneighbs(kappa, nr), 1)
+        np.partition(D, K, 1)
+        np.partition(D, K, 0)
+    except ValueError:
+        return True
+    return False
+
+
+@pytest.mark.parametrize("kappa", [0.0, 0.1, 0.5, 0.95, 3.0, 12.0])
+def test_ef_neighbour_error_matches_reference_partition(kappa):
+    """acoss._lib.ef_neighbour_error (the host check acoss_earlyfusion's wrapper runs before the
+    kernels) rejects exactly the block counts the reference's argpartition / partition reject: a
+    kappa >= 1 above a track's block count, or K >= either track's block count."""
+    from acoss import _lib
+    for K in (1, 3, 10):
+        for nq in range(1, 16):
+            for nr in range(1, 16):
+                err = _lib.ef_neighbour_error([nq], [nr], kappa, K)
+                assert (err is not None) == _reference_raises(nq, nr, kappa, K), (nq, nr, kappa, K)

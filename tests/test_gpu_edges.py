@@ -58,6 +58,28 @@ def test_earlyfusion_no_pairs():
     assert one.shape == (1, 4) and np.isfinite(one).all()
 
 
+def test_earlyfusion_rejects_neighbours_beyond_blocks():
+    """kappa >= 1 with int(kappa) >= a track's block count, or K >= a block count: the reference's
+    argpartition / partition raise ValueError (cross_recurrence.py:156, similarity_fusion.py:47);
+    so does the wrapper, before any kernel runs. A valid kappa >= 1 still scores."""
+    import torch
+    rng = np.random.default_rng(4)
+    nbs = [30, 12]
+    T = sum(nbs)
+    bank = {"mfccs": torch.as_tensor(rng.standard_normal((T, 1000), dtype=np.float32)).cuda(),
+            "ssms": torch.as_tensor(np.abs(rng.standard_normal((T, 1225), dtype=np.float32))).cuda(),
+            "chromas": torch.as_tensor(np.abs(rng.standard_normal((T, 480), dtype=np.float32))).cuda(),
+            "chroma_med": torch.as_tensor(np.abs(rng.standard_normal((2, 12), dtype=np.float32))).cuda(),
+            "off": torch.as_tensor(np.array([0, nbs[0]], np.int64)).cuda(),
+            "nb": torch.as_tensor(np.array(nbs, np.int32)).cuda(), "max_blocks": max(nbs)}
+    with pytest.raises(ValueError, match="out of bounds"):
+        _lib.earlyfusion(bank, np.array([[0, 1]], np.int32), kappa=12.0, K=5)   # 12 >= 12 columns
+    with pytest.raises(ValueError, match="out of bounds"):
+        _lib.earlyfusion(bank, np.array([[1, 0]], np.int32), kappa=0.1, K=12)   # K >= 12 rows
+    ok = _lib.earlyfusion(bank, np.array([[0, 1], [1, 0]], np.int32), kappa=11.0, K=5).cpu().numpy()
+    assert np.isfinite(ok).all()
+
+
 def test_ds_finish_one_by_one():
     import torch
     D = torch.full((1, 1), 3.0, dtype=torch.float32, device="cuda")

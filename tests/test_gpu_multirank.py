@@ -107,3 +107,28 @@ def test_earlyfusion_world2_equals_world1(datacos_mini, shard):
         assert d1[k].shape == (48, 48)
         assert np.count_nonzero(d1[k]) > 48 * 30, k
         np.testing.assert_array_equal(d2[k], d1[k], err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["Serra09", "LateFusionChen"])
+def test_benchmark_entry_point_world2(datacos_mini, name):
+    """coverid.benchmark (coverid.py:22-148) on two gloo ranks sharing the GPU:
+    Serra09 gathers Ds onto rank 0 only, LateFusionChen all-gathers it for the row-sharded SNF;
+    either way the matrices equal the world-1 run bit for bit, rank 0 alone writes the results
+    CSV (exactly one row per similarity type, the same rows as world 1), and no rank leaves a
+    memmap file in the cache directory."""
+    root, csv, fdir = datacos_mini
+    algo = "bench:" + name
+    d1 = _run(algo, 1, root, csv, fdir, "a")
+    d2 = _run(algo, 2, root, csv, fdir, "b", {"ACOSS_SNF_SHARD": "1"})
+    assert set(d1) == set(d2) and d1
+    for k in d1:
+        np.testing.assert_array_equal(d2[k], d1[k], err_msg=k)
+    rows = {}
+    for tag, world in (("a", 1), ("b", 2)):
+        cache = root / ("cache_%s_%s_w%d" % (algo, tag, world))
+        lines = (cache / ("results_mr_%s.csv" % name)).read_text().strip().splitlines()
+        assert lines[0].startswith("name,")
+        rows[world] = sorted(lines[1:])
+        assert sorted(r.split(",")[0] for r in rows[world]) == sorted("%s_%s" % (name, k) for k in d1), lines
+        assert not [f for f in os.listdir(cache) if "_dmat" in f], os.listdir(cache)
+    assert rows[1] == rows[2]

@@ -93,28 +93,107 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_worker(rank, world, port, csv, fdir, cache, out, symmetric):
+class PairwiseEvery(Pairwise):
+    """The same scorer with Ds assembled on every rank (the late-fusion subclasses' setting)."""
+    _Ds_on_every_rank = True
+
+
+def _rank_worker(rank, world, port, csv, fdir, cache, out, symmetric, every):
+    import json
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
-    a = Pairwise(csv, name="Fake%d" % rank, datapath=fdir, shortname="w", cachedir=cache)
+    cls = PairwiseEvery if every else Pairwise
+    a = cls(csv, name="Fake", datapath=fdir, shortname="w", cachedir=cache, similarity_types=["main", "other"])
     a.all_pairwise(symmetric=symmetric)
     np.save(out % rank, np.asarray(a.Ds["main"]))
+    stats = [a.getEvalStatistics(k) for k in ("main", "other")]
+    with open((out % rank) + ".json", "w") as f:
+        json.dump({"holds": a._holds_Ds, "stats": [[float(v) for v in st[:4]] + [list(map(int, st[4]))]
+                                                   for st in stats]}, f)
     dist.barrier()
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("every", [False, True])
 @pytest.mark.parametrize("symmetric", [True, False])
-def test_all_pairwise_gloo_world2_equals_world1(tmp_path, symmetric, monkeypatch):
+def test_all_pairwise_gloo_world2_equals_world1(tmp_path, symmetric, every, monkeypatch):
+    """Two gloo ranks through all_pairwise + getEvalStatistics: rank 0's Ds
+    equals the world-1 run bitwise; with the gather (every=False, Serra09 / SiMPle) rank 1 holds
+    no matrix, with the all-gather (every=True, the late-fusion algorithms) it holds the same one;
+    both ranks return the same statistics, exactly ONE results row per similarity type is written
+    (rank 0), and rank 1 leaves no memmap file behind."""
+    import json
     import torch.multiprocessing as mp
     monkeypatch.chdir(tmp_path)
     csv, fdir = _dataset(tmp_path, n_cliques=9)
     one = Pairwise(csv, name="One", datapath=fdir, shortname="w", cachedir=str(tmp_path / "c1"))
     one.all_pairwise(symmetric=symmetric)
+    ref_stats = [float(v) for v in one.getEvalStatistics("main")[:4]]
     out = str(tmp_path / "rank%d.npy")
-    mp.start_processes(_rank_worker, args=(2, _free_port(), csv, fdir, str(tmp_path / "c2"), out, symmetric),
+    cache = str(tmp_path / "c2")
+    mp.start_processes(_rank_worker, args=(2, _free_port(), csv, fdir, cache, out, symmetric, every),
                        nprocs=2, join=True, start_method="spawn")
-    for r in range(2):
-        np.testing.assert_array_equal(np.load(out % r), np.asarray(one.Ds["main"]))
+    np.testing.assert_array_equal(np.load(out % 0), np.asarray(one.Ds["main"]))
+    if every:
+        np.testing.assert_array_equal(np.load(out % 1), np.asarray(one.Ds["main"]))
+    else:
+        d1 = np.load(out % 1)  # rank 1 keeps only what it scored itself: its own stripe's rows
+        scored = np.flatnonzero(d1.any(1))
+        assert len(scored) and scored.min() > 0 and not np.array_equal(d1, np.asarray(one.Ds["main"]))
+    info = [json.load(open((out % r) + ".json")) for r in range(2)]
+    assert info[0]["holds"] and info[1]["holds"] == every
+    assert info[0]["stats"] == info[1]["stats"]
+    assert info[0]["stats"][0][:4] == ref_stats
+    rows = open("results_w_Fake.csv").read().strip().splitlines()
+    assert len(rows) == 3 and rows[0].startswith("name,"), rows  # header + one row per type
+    assert sorted(r.split(",")[0] for r in rows[1:]) == ["Fake_main", "Fake_other"], rows
+    assert not [f for f in os.listdir(cache) if ".rank" in f]
+
+
+def test_bind_local_device_rule(monkeypatch):
+    """acoss.distributed.bind_local_device under a mocked nccl job: a rank on the
+    default device is moved to LOCAL_RANK % device_count; a rank already on its GPU, or bound by
+    the caller to another non-default GPU, stays; gloo and uninitialised jobs bind nothing; without
+    LOCAL_RANK the launcher fallbacks, then rank % device_count, are used."""
+    import torch
+    import torch.distributed as dist
+    from acoss import distributed as D
+    state = {"cur": 0, "set": []}
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: state["cur"])
+
+    def set_device(d):
+        state["set"].append(d)
+        state["cur"] = d
+    monkeypatch.setattr(torch.cuda, "set_device", set_device)
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    backend = {"b": "nccl"}
+    monkeypatch.setattr(dist, "get_backend", lambda *a: backend["b"])
+    monkeypatch.setattr(dist, "get_rank", lambda *a: 11)
+    for v in D.LOCAL_RANK_VARS:
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    assert D.bind_local_device() == 3 and state["set"] == [3]
+    assert D.bind_local_device() == 3 and state["set"] == [3]        # already there: no rebind
+    monkeypatch.setenv("LOCAL_RANK", "13")
+    state["cur"] = 0
+    assert D.bind_local_device() == 5                               # 13 % 8
+    state["cur"], state["set"] = 6, []
+    assert D.bind_local_device() == 6 and state["set"] == []        # the caller's own binding stays
+    monkeypatch.delenv("LOCAL_RANK")
+    state["cur"] = 0
+    monkeypatch.setenv("SLURM_LOCALID", "2")
+    assert D.bind_local_device() == 2
+    monkeypatch.delenv("SLURM_LOCALID")
+    state["cur"] = 0
+    assert D.bind_local_device() == 3                               # rank 11 % 8
+    backend["b"] = "gloo"
+    state["cur"], state["set"] = 0, []
+    assert D.bind_local_device() is None and state["set"] == []
+    monkeypatch.setattr(dist, "is_initialized", lambda: False)
+    backend["b"] = "nccl"
+    assert D.bind_local_device() is None and state["set"] == []
 
 
 def test_resize_block_shapes():

@@ -113,6 +113,8 @@ def test_sharded_fusion_equals_world1(tmp_path, monkeypatch, world, n, L):
         else:
             assert all(p == plans[0] for p in plans), plans  # one decision, identical on every rank
             assert plans[0]["shard"] is (True if mode == "1" else plans[0]["rule_shard"])
+            # forced sharding pays for no probe; auto measures both operations
+            assert (plans[0]["t_step_replicated_ms"] is None) == (mode == "1")
             assert plans[0]["n"] == n and plans[0]["world"] == world
 
 
