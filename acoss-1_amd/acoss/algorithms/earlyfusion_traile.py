@@ -93,7 +93,9 @@ class EarlyFusion(CoverAlgorithm):
 
     def _compute_blocks(self, idx):
         """Block features of songs idx in one acoss_ef_block_features launch; cached in memory and
-        on disk like load_features."""
+        on disk like load_features. Under torch.distributed every rank computes the blocks on its
+        own GPU (one launch per 256 songs) and only rank 0 writes the disk cache, so W ranks do not
+        write the same 15,000 files W times."""
         tic = time.time()
         from ..features_io import load_many
         feats = load_many([self.filepaths[i] for i in idx],
@@ -106,13 +108,16 @@ class EarlyFusion(CoverAlgorithm):
         out = _lib.ef_block_features(chroma, mfcc, onsets, self.blocksize, self.mfccs_per_block,
                                      self.chromas_per_block)
         host = {k: out[k].cpu().numpy() for k in ("mfccs", "ssms", "chromas", "chroma_med")}
+        from .algorithm_template import _dist_info
+        write_cache = _dist_info()[1] == 0
         res = []
         for t, i in enumerate(idx):
             b0, nb = int(out["block_off"][t]), int(out["n_blocks"][t])
             bf = {"mfccs": host["mfccs"][b0:b0 + nb], "ssms": host["ssms"][b0:b0 + nb],
                   "chromas": host["chromas"][b0:b0 + nb], "chroma_med": host["chroma_med"][t]}
             self.all_block_feats[i] = bf
-            _save_feature_file("%s_%i.h5" % (self.get_cacheprefix(), i), bf)
+            if write_cache:
+                _save_feature_file("%s_%i.h5" % (self.get_cacheprefix(), i), bf)
             res.append(bf)
         if self.log_times:
             self.times['features'].append((time.time() - tic) / max(1, len(idx)))

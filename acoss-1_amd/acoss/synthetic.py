@@ -180,7 +180,7 @@ def pack(tracks):
 
 
 def write_feature_dataset(root, tracks, labels, with_mfcc=False, seed=SEED, beat_period=43, mfcc_shortfall=43,
-                          chroma_keys=("hpcp", "crema", "chroma_cens")):
+                          chroma_keys=("hpcp", "crema", "chroma_cens"), mfcc_from_chroma=False):
     """Write a dataset the plugin classes can read: '<root>/dataset.csv' (work_id, track_id)
     and one feature file per track at '<root>/features/<work_id>/<track_id>.npz' with the keys
     of the reference's feature dicts (README.md:93-114): the chroma_keys ('hpcp', 'crema',
@@ -188,9 +188,13 @@ def write_feature_dataset(root, tracks, labels, with_mfcc=False, seed=SEED, beat
     'madmom_features/onsets' (a fixed beat grid with jitter, up to the chroma's last frame). The
     reference extractor's mfcc_htk has about 43 frames fewer than its hpcp (22050-sample windows
     with validFrameThresholdRatio=1, acoss/features.py:884), so the last beats fall past the
-    MFCC's end as in real feature files. Returns (csv path, feature dir with trailing slash)."""
+    MFCC's end as in real feature files. mfcc_from_chroma: the MFCC frames are one fixed random
+    projection of the chroma frames plus noise (covers then share MFCC structure, so the MFCC
+    scores separate cliques too); otherwise independent noise. Returns (csv path, feature dir with
+    trailing slash)."""
     from .features_io import save_features
     rng = np.random.Generator(np.random.PCG64(seed))
+    proj = rng.standard_normal((20, 12)).astype(np.float32) if mfcc_from_chroma else None
     feat_dir = os.path.join(root, "features") + "/"
     rows = []
     for k, (t, lab) in enumerate(zip(tracks, labels)):
@@ -199,7 +203,11 @@ def write_feature_dataset(root, tracks, labels, with_mfcc=False, seed=SEED, beat
         f = dict({k: t for k in chroma_keys}, label=work, track_id=track)
         if with_mfcc:
             n = len(t)
-            f["mfcc_htk"] = rng.standard_normal((20, max(1, n - mfcc_shortfall))).astype(np.float32)
+            nm = max(1, n - mfcc_shortfall)
+            if proj is not None:
+                f["mfcc_htk"] = (proj @ t[:nm].T + 0.3 * rng.standard_normal((20, nm))).astype(np.float32)
+            else:
+                f["mfcc_htk"] = rng.standard_normal((20, nm)).astype(np.float32)
             beats = np.arange(0, n - 1, beat_period) + rng.integers(0, 3, size=len(range(0, n - 1, beat_period)))
             f["madmom_features"] = {"onsets": np.unique(np.clip(beats, 0, n - 1)).astype(np.int64)}
         save_features(feat_dir + work + "/" + track + ".h5", f)

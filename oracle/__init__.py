@@ -36,7 +36,8 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(_HERE, "crp_oracle.cpp")):
+        srcs = [os.path.join(_HERE, f) for f in ("crp_oracle.cpp", "ef_oracle.cpp")]
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
             build()
         L = ctypes.CDLL(LIB)
         L.or_stacked_len.restype = ctypes.c_int
@@ -74,6 +75,13 @@ def lib():
         L.or_ess_profile.argtypes = [_fp, ctypes.c_int, ctypes.c_int, _fp]
         L.or_ess_oti.restype = ctypes.c_int
         L.or_ess_oti.argtypes = [_fp, _fp, ctypes.c_int]
+        L.or_ef_csm.argtypes = [_fp, ctypes.c_int, _fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp, _fp, _fp]
+        L.or_ef_oti.restype = ctypes.c_int
+        L.or_ef_oti.argtypes = [_fp, _fp]
+        L.or_ef_binarize.argtypes = [_fp, ctypes.c_int, ctypes.c_int, ctypes.c_double, _u8p]
+        L.or_ef_batch.restype = ctypes.c_int
+        L.or_ef_batch.argtypes = [_fp, ctypes.c_int, _fp, ctypes.c_int, _fp, ctypes.c_int, _fp, _i64p, _i32p, _i32p,
+                                  ctypes.c_int64, ctypes.c_double, _dp, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -227,3 +235,42 @@ def simple_oti(A, B):
     A = np.ascontiguousarray(A, np.float64)
     B = np.ascontiguousarray(B, np.float64)
     return int(lib().or_simple_oti(_p(A, _dp), A.shape[1], _p(B, _dp), B.shape[1]))
+
+
+def ef_csm(X, Y, kind=0, med_a=None, med_b=None):
+    """EarlyFusion CSM in the canonical order of ef_oracle.cpp: kind 0 get_csm (euclid), 1
+    get_csm_blocked_oti with get_csm_cosine (the OTI of med_a / med_b; None: no roll)."""
+    X = np.ascontiguousarray(X, np.float32)
+    Y = np.ascontiguousarray(Y, np.float32)
+    D = np.zeros((X.shape[0], Y.shape[0]), np.float32)
+    ma = None if med_a is None else np.ascontiguousarray(med_a, np.float32)
+    mb = None if med_b is None else np.ascontiguousarray(med_b, np.float32)
+    lib().or_ef_csm(_p(X, _fp), X.shape[0], _p(Y, _fp), Y.shape[0], X.shape[1], int(kind),
+                    None if ma is None else _p(ma, _fp), None if mb is None else _p(mb, _fp), _p(D, _fp))
+    return D
+
+
+def ef_binarize(D, kappa):
+    """csm_to_binary with ties to the lowest column (ef_oracle.cpp)."""
+    D = np.ascontiguousarray(D, np.float32)
+    B = np.zeros(D.shape, np.uint8)
+    lib().or_ef_binarize(_p(D, _fp), D.shape[0], D.shape[1], float(kappa), _p(B, _u8p))
+    return B
+
+
+def ef_batch(bank, pairs, kappa=0.1, nthreads=0):
+    """(P, 3) float64 scores mfccs, ssms, chromas of EarlyFusion.similarity for (P, 2) pairs of a
+    packed block bank (dict of host arrays 'mfccs', 'ssms', 'chromas', 'chroma_med', 'off', 'nb'),
+    canonical order (ef_oracle.cpp)."""
+    mf = np.ascontiguousarray(bank["mfccs"], np.float32)
+    ss = np.ascontiguousarray(bank["ssms"], np.float32)
+    ch = np.ascontiguousarray(bank["chromas"], np.float32)
+    med = np.ascontiguousarray(bank["chroma_med"], np.float32)
+    off = np.ascontiguousarray(bank["off"], np.int64)
+    nb = np.ascontiguousarray(bank["nb"], np.int32)
+    pairs = np.ascontiguousarray(pairs, np.int32)
+    out = np.zeros((len(pairs), 3), np.float64)
+    lib().or_ef_batch(_p(mf, _fp), mf.shape[1], _p(ss, _fp), ss.shape[1], _p(ch, _fp), ch.shape[1], _p(med, _fp),
+                      _p(off, _i64p), _p(nb, _i32p), _p(pairs, _i32p), len(pairs), float(kappa), _p(out, _dp),
+                      int(nthreads))
+    return out

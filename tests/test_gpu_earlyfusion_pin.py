@@ -244,3 +244,30 @@ def test_earlyfusion_wave_csm_equals_lds_csm(tmp_path, nb, d_ssm):
         out[tag] = np.load(f)
     assert np.isfinite(out["wave"]).all()
     np.testing.assert_array_equal(out["wave"], out["lds"])
+
+
+def test_earlyfusion_scores_equal_canonical_oracle_on_float_blocks():
+    """On general float32 block features (not integer-exact) the GPU's mfccs / ssms / chromas
+    scores equal the canonical-order CPU oracle (oracle/ef_oracle.cpp, pinned against the
+    reference's golden CSMs / OTI / binarisation in tests/test_ef_oracle.py) on every pair: the
+    CSMs follow the same float32 order bit for bit, and binarisation and SW are exact. Ragged
+    block counts, K = 10, kappa = 0.1, and a kappa >= 1 count."""
+    import torch
+    from acoss import _lib
+    rng = np.random.default_rng(31)
+    nbs = [int(v) for v in rng.integers(12, 140, size=16)]
+    T, R = len(nbs), sum(nbs)
+    host = {"mfccs": rng.standard_normal((R, 1000), dtype=np.float32),
+            "ssms": np.abs(rng.standard_normal((R, 1225), dtype=np.float32)),
+            "chromas": np.abs(rng.standard_normal((R, 480), dtype=np.float32)),
+            "chroma_med": np.abs(rng.standard_normal((T, 12), dtype=np.float32)),
+            "nb": np.array(nbs, np.int32), "off": np.concatenate([[0], np.cumsum(nbs[:-1])]).astype(np.int64)}
+    bank = {k: torch.as_tensor(host[k]).cuda() for k in ("mfccs", "ssms", "chromas", "chroma_med", "off", "nb")}
+    bank["max_blocks"] = max(nbs)
+    pairs = np.array([(i, j) for i in range(T) for j in range(T) if i != j], np.int32)
+    for kappa in (0.1, 5.0):
+        got = _lib.earlyfusion(bank, pairs, kappa, 10).cpu().numpy()
+        ref = oracle.ef_batch(host, pairs, kappa)
+        for f, key in enumerate(("mfccs", "ssms", "chromas")):
+            bad = np.flatnonzero(got[:, f] != ref[:, f])
+            assert len(bad) == 0, (kappa, key, len(bad), pairs[bad[:5]], got[bad[:5], f], ref[bad[:5], f])
