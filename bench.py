@@ -62,6 +62,27 @@ PHASE_OPS = {"sweep": lambda s: s["sweep"] + 0.5 * s["selects"], "select_cols": 
              "dp_qmax": lambda s: s["dp"]}
 
 
+def build_id():
+    """Identity of the HIP build this tree runs: SHA-256 (first 16 hex) of the kernel sources and
+    their Makefile (acoss-1_amd/csrc, include/), and of the built library. profiles/profile.sh
+    records the same ids next to the counters, so bench.py can refuse PMC figures measured on
+    another build (VERDICT r04 #3)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    srcs = sorted(glob.glob(os.path.join(ROOT, "acoss-1_amd", "csrc", "*")) + glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for f in srcs:
+        h.update(os.path.relpath(f, ROOT).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    lib = os.path.join(ROOT, "acoss-1_amd", "acoss", "lib", "libacoss_hip.so")
+    lh = None
+    if os.path.exists(lib):
+        with open(lib, "rb") as fh:
+            lh = hashlib.sha256(fh.read()).hexdigest()[:16]
+    return {"src_sha16": h.hexdigest()[:16], "lib_sha16": lh}
+
+
 def log(msg):
     """Progress on stderr (the JSON line is the only stdout output)."""
     print("[bench %.1fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
@@ -554,15 +575,21 @@ def main():
                           "frac": round(ops / (v[0] * 1e-3) / 1e12 / PEAK_F32_TFLOPS, 4) if ops and v[0] > 0 else None}
         dom = max(kernels.items(), key=lambda kv: kv[1]["ms"])[0] if kernels else None
         achieved = opp * batch_pairs / (launch_ms * 1e-3) / 1e12
-        traffic, valu = None, None
+        traffic, valu, prof_build, prof_refused = None, None, None, []
+        build = build_id()
         for name, key in (("traffic_latest.json", "hbm_bytes_per_launch"), ("valu_latest.json", None)):
             tfile = os.path.join(ROOT, "profiles", name)
             if not os.path.exists(tfile):
                 continue
             try:  # measured by profiles/profile.sh on the same workload: only valid at that length/corpus
-                tj = json.load(open(tfile))
+                tj = json.load(open(tfile))  # and only for THIS build of the kernels
                 if tj.get("frames") != args.frames or tj.get("corpus", "bench") != args.corpus:
                     continue
+                if (tj.get("build") or {}).get("src_sha16") != build["src_sha16"]:
+                    prof_refused.append("%s: measured on build %s, this is %s" % (
+                        name, (tj.get("build") or {}).get("src_sha16"), build["src_sha16"]))
+                    continue
+                prof_build = tj.get("build")
                 if key:
                     traffic = tj.get(key)
                 else:
@@ -578,7 +605,14 @@ def main():
                     "one_stream_call_ms": round(call1_ms, 3) if call1_ms else None,
                     "kernel_ms_sum_one_stream": round(kernel_ms_sum, 3) if kernel_ms_sum else None,
                     "dominant_kernel": dom, "kernels": kernels,
-                    "valu_issue": valu}
+                    "valu_issue": valu,
+                    # the Serra09 path issues no MFMA (its 12-deep Gram runs as packed-FP32 VALU,
+                    # DESIGN.md §3); gram_frac = the §8d MFMA-shaped share (2*12*M*N flops/pair)
+                    # at this rate against the fp32 matrix peak
+                    "mfma_frac": 0.0,
+                    "gram_frac": round(2.0 * 12 * args.frames * args.frames * batch_pairs / (launch_ms * 1e-3)
+                                       / 1e12 / PEAK_F32_TFLOPS, 4),
+                    "traffic_build": prof_build, "traffic_refused": prof_refused or None}
         if traffic:  # the same call against the HBM roofline of the bytes it actually moves
             bpp = traffic / batch_pairs
             bound = 8e12 / bpp
@@ -633,6 +667,7 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu,
             "speedup_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
             "other_paths": paths,
+            "build": build,
             "launch": {"world": world, "device_count": n_dev, "backend": backend if world > 1 else None,
                        "launcher": os.environ.get("ACOSS_BENCH_LAUNCHER", "external" if world > 1 else None)},
         }

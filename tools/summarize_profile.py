@@ -40,6 +40,8 @@ for part in ("sq", "fetch", "write"):
             continue
         k = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("acoss::", "")
         out[k][r["Counter_Name"]] = out[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+bfile = os.path.join(src, "build.json")
+build = json.load(open(bfile)) if os.path.exists(bfile) else None
 tot = 0.0
 for k, v in out.items():
     hbm = 1024.0 * (2.0 * v.get("FETCH_SIZE", 0.0) + v.get("WRITE_SIZE", 0.0))
@@ -47,7 +49,7 @@ for k, v in out.items():
     tot += hbm
 json.dump(out, open(os.path.join(rdir, tag + "_pmc.json"), "w"), indent=1, sort_keys=True)
 json.dump({"source": os.path.join(rdir, tag + "_pmc.json"), "calls": calls, "frames": frames, "corpus": corpus,
-           "hbm_bytes_per_launch": tot / calls,
+           "build": build, "hbm_bytes_per_launch": tot / calls,
            "note": "sum over all acoss kernels of 1024*(2*FETCH_SIZE+WRITE_SIZE) / acoss_crp_align calls"},
           open(os.path.join("profiles", "traffic_latest.json"), "w"), indent=1)
 # per-kernel durations (kernel trace, one stream) and VALU-issue fractions
@@ -67,7 +69,7 @@ for k, d in dur.items():
                    valu_issue_frac=(instr / (d["total_ms"] * 1e-3 * PEAK_WAVE_INSTR)) if d["total_ms"] > 0 else None)
 ksum = sum(d["total_ms"] for d in dur.values()) / calls
 json.dump({"source": os.path.join(rdir, tag + "_kernel_stats.csv") + " + " + os.path.join(rdir, tag + "_pmc.json"),
-           "calls": calls, "frames": frames, "corpus": corpus, "streams": 1,
+           "calls": calls, "frames": frames, "corpus": corpus, "streams": 1, "build": build,
            "kernel_ms_per_call": ksum, "kernels": valu,
            "peak_wave_instr_per_s": PEAK_WAVE_INSTR},
           open(os.path.join("profiles", "valu_latest.json"), "w"), indent=1)
