@@ -988,9 +988,6 @@ struct Stage {
   size_t sel_lds = 0, pan_lds = 0;
 };
 
-// Default slots per XCD of the row-major key-plane ring (ACOSS_HR_RING overrides; 0 = off).
-constexpr int kHrRingSlots = 0;
-
 int prepare_stage(int m, int ld, Stage* st) {
   st->R = pick_R(m, ld);
   if (st->R <= 0) {
@@ -1204,15 +1201,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
     const int v = e ? atoi(e) : 2;
     return v < 1 ? 1 : (v > 3 ? 3 : v);
   }();
-  // fused launches (k_sweep_cols9: a sub-batch's sweep and an earlier one's column select in one
-  // grid) instead of separate kernels: opt-in, ACOSS_SPLIT_FUSED=1 (with >= 2 streams; measured 82.2k vs 81.3k pairs/s at exactly 2000 frames, but
-  // separate kernels ran faster at every other shape tried: 718k vs 608k at 500 frames, 231k vs
-  // 229k at 1000, 289k vs 275k for U[250, 1250], 71.8k vs 70.9k for U[1800, 2200])
-  const char* fused_env = getenv("ACOSS_SPLIT_FUSED");
-  const bool fused = split && nbuf >= 2 && fused_env && fused_env[0] == '1';
-  // fused launches alternate between two streams, launch k pairing sub-batch k's sweep with
-  // sub-batch k-2's select (same stream): four plane buffers keep every writer and reader apart
-  const int nkb = fused ? 4 : nbuf;
+  const int nkb = nbuf;
   char* ws = static_cast<char*>(workspace(1, slot * nb_alloc + (split ? nkb * sub_pair * sub : 0) + 8192));
   if (!ws) return ACOSS_E_HIP;
   size_t o = 0;
@@ -1230,39 +1219,14 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
   uint32_t* w_mask = reinterpret_cast<uint32_t*>(carve(4 * mask_stride * nb_alloc));
   float4* w_bnd = reinterpret_cast<float4*>(carve(16 * bnd_stride * nb_alloc));
   float* w_yrot = reinterpret_cast<float*>(carve(4 * yrot_stride * nb_alloc));
-  void* w_kpl[4] = {nullptr, nullptr, nullptr, nullptr};
-  uint32_t* w_rt[4] = {nullptr, nullptr, nullptr, nullptr};
+  void* w_kpl[3] = {nullptr, nullptr, nullptr};
+  uint32_t* w_rt[3] = {nullptr, nullptr, nullptr};
   for (int b = 0; split && b < nkb; ++b) {
     w_kpl[b] = static_cast<void*>(carve(4 * (size_t)kstride * sub));
     w_rt[b] = reinterpret_cast<uint32_t*>(carve(4 * (size_t)mask_stride * sub));
   }
-  // row-major key plane as per-XCD rings of strip slots (HrRing, crp_split.hip): ACOSS_HR_RING =
-  // slots per XCD (a power of two; 0 = per-pair planes). One ring + its counters per stream.
-  HrRing rings[3] = {};
-  if (split) {
-    int S = kHrRingSlots;
-    if (const char* e = getenv("ACOSS_HR_RING")) S = atoi(e);
-    if (S < 0 || (S & (S - 1)) != 0 || S > 4096) S = kHrRingSlots;
-    if (S > 0) {
-      const size_t ring_elems = (size_t)8 * S * 32 * ldk;               // uint16
-      const size_t ctl_bytes = align_up((size_t)8 * 16 * 8 + (size_t)8 * S * 4, 256);
-      const size_t per = align_up(ring_elems * 2, 256) + ctl_bytes;
-      char* rw = static_cast<char*>(workspace(14, per * nbuf));
-      if (!rw) return ACOSS_E_HIP;
-      // the ticket / generation counters start at zero on EVERY call that uses the ring (a few KB,
-      // stream-ordered before the sub-batches, whose side streams wait on an event recorded on s
-      // after it): no state carried between calls, devices or an aborted launch
-      for (int b = 0; b < nbuf; ++b) {
-        char* base = rw + per * b;
-        char* ctl = base + align_up(ring_elems * 2, 256);
-        rings[b] = HrRing{reinterpret_cast<uint16_t*>(base), reinterpret_cast<unsigned long long*>(ctl),
-                          reinterpret_cast<unsigned*>(ctl + 8 * 16 * 8), S};
-        ACOSS_HIP_CHECK(hipMemsetAsync(ctl, 0, ctl_bytes, s));
-      }
-    }
-  }
   hipStream_t ss[3] = {s, s, s};
-  for (int b = 1; split && b < (fused ? 2 : nbuf); ++b) {
+  for (int b = 1; split && b < nbuf; ++b) {
     ss[b] = side_stream(b - 1);
     if (!ss[b]) {
       set_error("could not create the side stream");
@@ -1282,42 +1246,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
                        yrot_stride);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_OTI, s);
-    if (split && fused) {
-      // launch k (stream k % 2): sub-batch k's sweep (plane buffer k % 4) with sub-batch k - 2's
-      // column select (buffer (k - 2) % 4, swept by launch k - 2 on the same stream); two more
-      // launches finish the last two selects
-      const int nsb = (int)((nb + sub - 1) / sub);
-      hipEvent_t e0 = sync_event(0);
-      ACOSS_HIP_CHECK(hipEventRecord(e0, s));
-      ACOSS_HIP_CHECK(hipStreamWaitEvent(ss[1], e0, 0));
-      std::vector<SplitSide> sides((size_t)nsb);
-      for (int k = 0; k < nsb + 2; ++k) {
-        SplitSide cur{}, old{};
-        cur.nb = old.nb = 0;
-        if (k < nsb) {
-          const int s0 = (int)(k * sub);
-          const int ns = (nb - s0) < sub ? (nb - s0) : (int)sub;
-          const int b = k & 3;
-          cur = SplitSide{CrpBatch{feats, X2, track_off, track_len, NX, ldn, pb + 2 * s0, w_oti + s0, w_dims + s0, m,
-                                   tau, w_yrot + (size_t)s0 * yrot_stride, yrot_stride},
-                          ns, w_kpl[b], rings[b & 1], w_rt[b],
-                          w_thr_r + (size_t)s0 * thr_stride, w_T_r + (size_t)s0 * thr_stride,
-                          w_thr_c + (size_t)s0 * thr_stride, w_T_c + (size_t)s0 * thr_stride,
-                          w_mask + (size_t)s0 * mask_stride};
-          sides[(size_t)k] = cur;
-        }
-        if (k >= 2) old = sides[(size_t)(k - 2)];
-        if (cur.nb == 0 && old.nb == 0) continue;
-        if (cur.nb == 0) cur.B = old.B;
-        if (old.nb == 0) old.B = cur.B;
-        if ((rc = launch_crp_split_fused(cur, old, L, params->kappa, ldk, kstride, thr_stride, mask_stride, ld,
-                                         ss[k & 1])))
-          return rc;
-      }
-      hipEvent_t e1 = sync_event(1);  // the DP (caller's stream) needs both streams' launches
-      ACOSS_HIP_CHECK(hipEventRecord(e1, ss[1]));
-      ACOSS_HIP_CHECK(hipStreamWaitEvent(s, e1, 0));
-    } else if (split) {
+    if (split) {
       const int nsb = (int)((nb + sub - 1) / sub);     // sub-batches of this batch
       const int nst = nbuf < nsb ? nbuf : nsb;         // streams they rotate over
       if (nst > 1) {  // the side streams start after this batch's OTI / roll on the caller's stream
@@ -1331,7 +1260,7 @@ extern "C" int acoss_crp_align(const float* feats, const int64_t* track_off, con
         const int b = k % nst;
         CrpBatch Bs{feats, X2, track_off, track_len, NX, ldn, pb + 2 * s0, w_oti + s0, w_dims + s0, m, tau,
                     w_yrot + (size_t)s0 * yrot_stride, yrot_stride};
-        if ((rc = launch_crp_split(Bs, ns, L, params->kappa, w_kpl[b], rings[b], ldk, kstride, w_rt[b],
+        if ((rc = launch_crp_split(Bs, ns, L, params->kappa, w_kpl[b], ldk, kstride, w_rt[b],
                                    w_thr_r + (size_t)s0 * thr_stride, w_T_r + (size_t)s0 * thr_stride,
                                    w_thr_c + (size_t)s0 * thr_stride, w_T_c + (size_t)s0 * thr_stride, thr_stride,
                                    w_mask + (size_t)s0 * mask_stride, mask_stride, ld, ss[b])))

@@ -20,18 +20,6 @@ struct CrpBatch {
   int64_t yrot_stride;   // floats between consecutive pairs in yrot
 };
 
-// Row-major key plane as a ring of strip slots per XCD (crp_split.hip k_sweep_rows9): a block
-// takes a ticket from its XCD's counter, waits for the slot's previous owner (ticket - slots) to
-// release it, and only ever shares the slot with blocks of the same XCD (one L2, coherent), so the
-// 2 B/cell row-major plane cycles through cache instead of streaming to HBM. slots = 0: off (the
-// plane is per pair, as the strip-major one).
-struct HrRing {
-  uint16_t* base;                // 8 XCDs x slots x (32 rows x ldk) uint16
-  unsigned long long* ticket;    // 8 counters, one 128-B line each (stride 16)
-  unsigned* gen;                 // 8 x slots release counts
-  int slots;                     // per XCD, a power of two (0 = off)
-};
-
 // Constant-address-space view of read-only global data: wave-uniform loads through it
 // become scalar (s_load) loads whose values live in SGPRs.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -43,27 +31,12 @@ typedef __attribute__((address_space(4))) const f32x4 cfloat4;
 int launch_mask9(const CrpBatch& B, int nb, int L, const float* Trow, const float* Tcol, int64_t thr_stride,
                  uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s);
 
-// Three-kernel CRP around one sweep (crp_split.hip); 1 = not covered.
-// kplanes: 4 planes of nb*kstride uint16 (key high/low halves, row- and column-major).
-int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, const HrRing& ring, int ldk,
+// Two-kernel CRP around one sweep (crp_split.hip); 1 = not covered.
+// kplanes: 2 planes of nb*kstride uint16 (16-bit key prefixes, row-major and strip-major).
+int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, int ldk,
                      int64_t kstride,
                      uint32_t* RT, float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride,
                      uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s);
-
-// One side of a fused split launch (launch_crp_split_fused): a sub-batch of nb pairs (nb = 0:
-// none), its key planes and row-threshold words, and the outputs of its kernel (the row
-// thresholds for the sweep side; the column thresholds and CRP words for the select side).
-struct SplitSide {
-  CrpBatch B;
-  int nb;
-  void* kpl;
-  HrRing ring;
-  uint32_t* RT;
-  float *thr_r, *T_r, *thr_c, *T_c;
-  uint32_t* maskT;
-};
-int launch_crp_split_fused(const SplitSide& S, const SplitSide& C, int L, float kappa, int ldk, int64_t kstride,
-                           int64_t thr_stride, int64_t mask_stride, int ld, hipStream_t s);
 
 int launch_select16(bool trans, const CrpBatch& B, int nb, int L, float kappa, float* thr, float* T,
                     int64_t thr_stride, hipStream_t s);

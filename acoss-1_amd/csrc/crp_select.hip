@@ -156,14 +156,6 @@ __device__ __forceinline__ unsigned full_key_fast(const SelCtx& C, const float* 
 
 // ---- per-wave helpers ----
 
-// Diagnostic stamps (ACOSS_DEBUG_STAMPS): wave 0 of each block adds the cycles of each
-// phase into dbg[0..7]. The branch is uniform; with dbg == nullptr no stamp executes.
-__device__ __forceinline__ unsigned long long stamp() {
-  unsigned long long t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
-
 // ---- per-row select on 16-bit key prefixes held in registers ----
 // Keys of one row as seen by one lane: lane l holds elements l + 64q (0xffffffff = none).
 template <int KPL>
@@ -266,10 +258,8 @@ constexpr int kCand = 1024;  // block-wide candidate list capacity
 
 template <bool TRANS>
 __device__ __forceinline__ void select_body(const SelCtx& C, uint16_t* K16, float* Ys, float* Ns, float kappa, float* thr_out,
-                            float* T_out, int ablate, unsigned long long* dbg) {
+                            float* T_out) {
   const int t = threadIdx.x;
-  unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
-  if (dbg) ts0 = stamp();
   // own stacked norms of the stripe: wave-uniform, loaded once (SGPRs)
   float nown[kR];
 #pragma unroll
@@ -278,8 +268,7 @@ __device__ __forceinline__ void select_body(const SelCtx& C, uint16_t* K16, floa
     nown[r] = *(const __attribute__((address_space(4))) float*)(C.Nown + i);
   }
   // ---- sweep: parallelogram panels of 256 diagonals ----
-  // (ablate: debug knob ACOSS_DEBUG_ABLATE, 1 = skip the sweep, 2 = skip the selects)
-  for (int j0 = -(kR - 1); j0 < ((ablate & 1) ? -(kR - 1) : C.n_in_s); j0 += kW) {
+  for (int j0 = -(kR - 1); j0 < C.n_in_s; j0 += kW) {
     __syncthreads();
     for (int e = t; e < kYRows * 3; e += kW) {  // stage inner frames (float4 pieces)
       const int b = e / 3, piece = e - b * 3;
@@ -343,7 +332,6 @@ __device__ __forceinline__ void select_body(const SelCtx& C, uint16_t* K16, floa
     }
   }
   __syncthreads();
-  if (dbg) ts1 = stamp();
   // ---- selects ----
   // LDS scratch (aliases the panel buffers): own frames | candidate list | row records | counter
   float* Xown = Ys;
@@ -364,7 +352,7 @@ __device__ __forceinline__ void select_body(const SelCtx& C, uint16_t* K16, floa
   const float lo_f = floorf(q), hi_f = ceilf(q);
   const int lo = (int)lo_f, hi = (int)hi_f;
   const bool regs = n <= 64 * 32;
-  const int nrows = (ablate & 2) ? 0 : C.rows;
+  const int nrows = C.rows;
   // phase A (per wave): 16-bit prefixes of both order statistics; candidates collected
   for (int r = w; r < nrows; r += 4) {
     const uint16_t* row = K16 + r * C.ld16;
@@ -413,7 +401,6 @@ __device__ __forceinline__ void select_body(const SelCtx& C, uint16_t* K16, floa
     if (lane == 0) rs[r] = sel;
   }
   __syncthreads();
-  if (dbg) ts2 = stamp();
   // phase B (block): exact keys of every collected candidate, one per thread, in one round
   const int nc = min(*ncand, kCand);
   for (int e = t; e < nc; e += kW) {
@@ -422,7 +409,6 @@ __device__ __forceinline__ void select_body(const SelCtx& C, uint16_t* K16, floa
     cand[e] = (int)full_key_fast<TRANS>(C, Xown, C.i0 + r, j, true);
   }
   __syncthreads();
-  if (dbg) ts3 = stamp();
   // phase C (per wave): rank inside the groups, interpolate, squared-domain threshold
   for (int r = w; r < nrows; r += 4) {
     const int srow = __builtin_amdgcn_readfirstlane(C.i0 + r);
@@ -480,23 +466,11 @@ __device__ __forceinline__ void select_body(const SelCtx& C, uint16_t* K16, floa
       T_out[srow] = sq_threshold(thr);
     }
   }
-  if (dbg) {
-    __syncthreads();
-    const unsigned long long ts4 = stamp();
-    if (t == 0) {
-      atomicAdd(dbg + 0, ts1 - ts0);
-      atomicAdd(dbg + 1, ts2 - ts1);
-      atomicAdd(dbg + 2, ts3 - ts2);
-      atomicAdd(dbg + 3, ts4 - ts3);
-      atomicAdd(dbg + 4, 1ull);
-    }
-  }
 }
 
 template <bool TRANS>
 __global__ __launch_bounds__(256, 2) void k_crp_select16(CrpBatch B, int ld16, float kappa, float* __restrict__ thr,
-                                                         float* __restrict__ Tq, int64_t thr_stride, int ablate,
-                                                         unsigned long long* dbg) {
+                                                         float* __restrict__ Tq, int64_t thr_stride) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem8[];
   const int p = blockIdx.y;
   const int2 dm = B.dims[p];
@@ -522,7 +496,7 @@ __global__ __launch_bounds__(256, 2) void k_crp_select16(CrpBatch B, int ld16, f
   uint16_t* K16 = reinterpret_cast<uint16_t*>(smem8);
   float* Ys = reinterpret_cast<float*>(smem8 + align_up((size_t)kR * ld16 * 2, 16));
   float* Ns = Ys + kYRows * 12;
-  select_body<TRANS>(C, K16, Ys, Ns, kappa, thr + (size_t)p * thr_stride, Tq + (size_t)p * thr_stride, ablate, dbg);
+  select_body<TRANS>(C, K16, Ys, Ns, kappa, thr + (size_t)p * thr_stride, Tq + (size_t)p * thr_stride);
 }
 
 size_t select16_lds(int ld16) {
@@ -543,25 +517,12 @@ int launch_select16(bool trans, const CrpBatch& B, int nb, int L, float kappa, f
                          : reinterpret_cast<const void*>(k_crp_select16<false>);
   if (lds > 64 * 1024) ACOSS_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const dim3 grid((L + kR - 1) / kR, nb);
-  static const int ablate = getenv("ACOSS_DEBUG_ABLATE") ? atoi(getenv("ACOSS_DEBUG_ABLATE")) : 0;
-  unsigned long long* dbg = nullptr;
-  if (getenv("ACOSS_DEBUG_STAMPS")) dbg = static_cast<unsigned long long*>(workspace(9, 256));
   if (trans)
-    hipLaunchKernelGGL(k_crp_select16<true>, grid, dim3(256), lds, s, B, ld16, kappa, thr, T, thr_stride, ablate, dbg);
+    hipLaunchKernelGGL(k_crp_select16<true>, grid, dim3(256), lds, s, B, ld16, kappa, thr, T, thr_stride);
   else
-    hipLaunchKernelGGL(k_crp_select16<false>, grid, dim3(256), lds, s, B, ld16, kappa, thr, T, thr_stride, ablate, dbg);
+    hipLaunchKernelGGL(k_crp_select16<false>, grid, dim3(256), lds, s, B, ld16, kappa, thr, T, thr_stride);
   ACOSS_LAUNCH_CHECK();
   return ACOSS_OK;
 }
 
 }  // namespace acoss
-
-// Diagnostic: read and clear the stamp sums (ACOSS_DEBUG_STAMPS builds only).
-extern "C" int acoss_debug_stamps(unsigned long long* out8) {
-  void* d = acoss::workspace(9, 256);
-  if (!d) return ACOSS_E_HIP;
-  if (hipDeviceSynchronize() != hipSuccess) return ACOSS_E_HIP;
-  if (hipMemcpy(out8, d, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return ACOSS_E_HIP;
-  if (hipMemset(d, 0, 256) != hipSuccess) return ACOSS_E_HIP;
-  return ACOSS_OK;
-}

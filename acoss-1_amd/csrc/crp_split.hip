@@ -25,12 +25,10 @@
 
 #include "crp_internal.hpp"
 
-#ifndef ACOSS_LW_SELECT  // (ACOSS_LW_SELECT: the round-3 compare/select placement, for A/B)
 // v_writelane_b32 through the LLVM intrinsic (hipcc has no builtin for it), so the compiler's
 // hazard recognizer inserts the wait state between the ballot's SGPR write and the writelane
 // (the inline-asm form of round 3 lacked it and produced wrong words)
 __device__ int acoss_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
-#endif
 
 namespace acoss {
 
@@ -41,23 +39,6 @@ constexpr int kMS = 9;
 // 16-bit prefix of "no element": above every real prefix (finite keys >= +0 have prefixes <= 0x7f80)
 constexpr unsigned kNone = 0x7fffu;
 
-#ifdef ACOSS_STAMPS  // diagnostic builds only: per-phase cycle sums of the fused sweep
-__device__ unsigned long long d_sweep_stamps[48];
-__device__ __forceinline__ unsigned long long sstamp() {
-  unsigned long long t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
-#define ACOSS_STAMP(v) const unsigned long long v = sstamp()
-#define ACOSS_STAMP_ADD(slot, a, b) \
-  if ((threadIdx.x & 63) == 0) atomicAdd(&d_sweep_stamps[slot], (b) - (a))
-#define ACOSS_COUNT(slot, v) \
-  if ((threadIdx.x & 63) == 0) atomicAdd(&d_sweep_stamps[slot], (unsigned long long)(v))
-#else
-#define ACOSS_COUNT(slot, v)
-#define ACOSS_STAMP(v)
-#define ACOSS_STAMP_ADD(slot, a, b)
-#endif
 
 struct PairView {
   const float* X;   // query frames
@@ -95,7 +76,6 @@ constexpr int kSR = 32;                       // rows per strip
 struct KeyPlanes {
   uint16_t* hr;
   uint16_t* hc;
-  HrRing ring;
 };
 
 // Exact key of cell (i, j), recomputed in the sweep's canonical order: 12-term fmaf chain per
@@ -120,9 +100,6 @@ __device__ __forceinline__ float gram12(const f32x4& x0, const f32x4& x1, const 
 }
 
 __device__ __forceinline__ float cell_gram(const PairView& V, int fq, int fr) {
-#ifdef ACOSS_ABL_NOGRAM  // timing ablation only (wrong results): no frame loads in the recompute
-  return (float)(fq * 3 + fr);
-#endif
   const f32x4* x = reinterpret_cast<const f32x4*>(V.X + (size_t)fq * 12);
   const f32x4* y = reinterpret_cast<const f32x4*>(V.Yr + (size_t)fr * 12);
   const f32x4 x0 = x[0], x1 = x[1], x2 = x[2], y0 = y[0], y1 = y[1], y2 = y[2];
@@ -161,9 +138,6 @@ typedef __attribute__((address_space(1))) uint16_t gu16;
 // Store at a 32-bit byte offset from an SGPR base: global_store_short v_off, v, s[base] (saddr
 // form; a u16 element index would need a 64-bit address per store).
 __device__ __forceinline__ void st_u16(gu16* base, unsigned idx, unsigned v) {
-#ifdef ACOSS_ABL_NOHR  // timing ablation only (wrong results): no row-major plane stores
-  return;
-#endif
   typedef __attribute__((address_space(1))) char gchar;
   *(gu16*)((gchar*)base + idx * 2u) = (uint16_t)v;
 }
@@ -200,11 +174,7 @@ __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int str
   const int rows = PARTIAL ? min(kSR, V.Mp - i0) : kSR;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#ifdef ACOSS_ABL_HCRING  // timing ablation only (wrong results): strip-major plane as a ring of pairs
-  uint16_t* Hc = K.hc + (size_t)(p % ACOSS_ABL_HCRING) * kstride;
-#else
   uint16_t* Hc = K.hc + (size_t)p * kstride;
-#endif
   const float* X2b = V.X2 + (size_t)i0 * 24;
   const float* Nq0 = V.NXq + i0;
   auto nqr = [&](int r) {  // row norm: a scalar load at a compile-time offset
@@ -300,7 +270,6 @@ __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int str
         }
       }
     }
-#ifndef ACOSS_HC_LANE_STORES
     // strip-major stores in 64-byte runs: a 4 x 4 transpose of the 16-byte pieces inside each lane
     // quad (two DPP butterfly stages per piece word), then store k: lane b + m (b = lane & ~3)
     // writes piece m of lane b + k's column, so a quad writes one column's 64 bytes contiguously
@@ -333,24 +302,6 @@ __device__ __forceinline__ void sweep_body_sys(const PairView& V, int p, int str
         if (b + k >= kMS - 1 && c < V.Np)
           reinterpret_cast<uint4*>(Hc + ((size_t)strip * ldc + c) * kSR)[m] = make_uint4(T[k][0], T[k][1], T[k][2], T[k][3]);
       }
-    }
-    if (false) {
-#elif defined(ACOSS_ABL_NOHC)  // timing ablation only (wrong results): no strip-major plane stores
-    if (hw[0] == 0x12345678u && hw[15] == 0x9abcdef0u) {
-#else
-    if (valid) {
-#endif
-      uint4* dh = reinterpret_cast<uint4*>(Hc + ((size_t)strip * ldc + col) * kSR);
-#ifdef ACOSS_HC_NT  // streaming stores: the column plane is read back by another kernel, later
-      typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-      u32x4v* dv = reinterpret_cast<u32x4v*>(dh);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        __builtin_nontemporal_store(u32x4v{hw[4 * q], hw[4 * q + 1], hw[4 * q + 2], hw[4 * q + 3]}, dv + q);
-#else
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dh[q] = make_uint4(hw[4 * q], hw[4 * q + 1], hw[4 * q + 2], hw[4 * q + 3]);
-#endif
     }
   }
   // kNone over [N', align32(N')) of every row: the row select's last 32-element run then needs
@@ -434,12 +385,7 @@ struct HistAddr {
   }
 };
 __device__ __forceinline__ void hist_add(unsigned* hist, const HistAddr& A, unsigned c, bool in) {
-#ifndef ACOSS_HIST_SINK_PV  // the 16-bit prefix forms keep the masked add (the sink: -6 % at 500 frames)
   if (in) __hip_atomic_fetch_add(hist + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#else
-  const unsigned a = in ? A.hb + 4u * c : A.sk;
-  __hip_atomic_fetch_add((lds_u32*)(size_t)a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#endif
 }
 
 // The rank search of hist_rank on a line's 7-bit window codes (w8: four codes per word; window
@@ -456,21 +402,6 @@ __device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned 
   __builtin_amdgcn_wave_barrier();
   unsigned below = 0;
   const unsigned cmin = base8 == 0u ? 0u : 1u;  // code 0 is exact only when base8 == 0
-#ifdef ACOSS_HIST_MASKED
-  if (cmin) {
-#pragma unroll
-    for (int h = 0; h < NW; ++h) below = __builtin_popcount((0x80808080u - w8[h]) & 0x80808080u) + below;
-  }
-#pragma unroll
-  for (int h = 0; h < NW; ++h) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const unsigned c = (w8[h] >> (8 * k)) & 0x7fu;
-      if (c - cmin < 127u - cmin) __hip_atomic_fetch_add(hist + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    }
-  }
-  const int below_tot = wave_sum((int)below);
-#else
   // every code below 127 into its bin, code 0 included (the elements at or below base8, exact
   // only when base8 == 0: a rank landing in bin 0 otherwise returns false below), so no separate
   // count of the elements under the window; code 127 to this lane's sink. Per code: the byte (7-bit
@@ -487,7 +418,6 @@ __device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned 
   }
   const int below_tot = 0;
   (void)below;
-#endif
   __builtin_amdgcn_wave_barrier();
   const uint2 hv = reinterpret_cast<const uint2*>(hist)[lane];
   const int sl = (int)(hv.x + hv.y);
@@ -500,9 +430,7 @@ __device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned 
   const int Es = __builtin_amdgcn_readlane(E, src);
   const int h0 = __builtin_amdgcn_readlane((int)hv.x, src), h1 = __builtin_amdgcn_readlane((int)hv.y, src);
   const bool second = r >= Es + h0;
-#ifndef ACOSS_HIST_MASKED
   if (cmin && src == 0 && !second) return false;  // bin 0 of a window above 0: not an exact prefix
-#endif
   *P = base8 + 2u * (unsigned)src + (second ? 1u : 0u);
   *less = below_tot + Es + (second ? h0 : 0);
   *le = *less + (second ? h1 : h0);
@@ -564,14 +492,7 @@ struct Line {
     unsigned w[KPL / 2];
 #pragma unroll
     for (int q = 0; q < KPL / 8; ++q) {
-#ifdef ACOSS_HC_NTLOAD  // column plane read once: streaming loads, so they do not evict the frames from L2
-      typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-      const u32x4v vv = STORED_SPLIT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(src) + q)
-                                     : reinterpret_cast<const u32x4v*>(src)[q];
-      const uint4 v = make_uint4(vv.x, vv.y, vv.z, vv.w);
-#else
       const uint4 v = reinterpret_cast<const uint4*>(src)[q];
-#endif
       w[4 * q + 0] = v.x;
       w[4 * q + 1] = v.y;
       w[4 * q + 2] = v.z;
@@ -710,18 +631,15 @@ struct Line {
   __device__ __forceinline__ unsigned min_greater_lane(unsigned x) const { return swar_min_greater(pv, x); }
   __device__ __forceinline__ unsigned min_greater(unsigned x) const { return wave_min_u32(min_greater_lane(x)); }
   static constexpr int kHalves = 1;
-#ifndef ACOSS_NO_HIST_LONG
   // LineS::hist_rank for the 32 elements per lane of a long line (ACOSS_NO_HIST_LONG: the search
   // alone, for A/B)
   static constexpr bool kHist = true;
   __device__ __forceinline__ bool hist_rank(unsigned hint, int rho, unsigned* hist, unsigned* P, int* le,
                                             int* less, unsigned* hbase) const {
-#ifndef ACOSS_HIST_PV  // (ACOSS_HIST_PV: bin the 16-bit prefixes instead, for A/B)
     if (win) {  // the window codes around the same hint (built before every hinted search)
       *hbase = base8;
       return hist_rank_w8(w8, base8, rho, hist, P, le, less);
     }
-#endif
     const int lane = threadIdx.x & 63;
     const unsigned base = hint > 64u ? hint - 64u : 0u;
     *hbase = base;
@@ -760,9 +678,6 @@ struct Line {
     *le = *less + (second ? h1 : h0);
     return true;
   }
-#else
-  static constexpr bool kHist = false;
-#endif
 };
 
 // Short lines (up to 64 KQ elements): lane l holds elements l + 64 q, q < KQ,
@@ -916,14 +831,12 @@ struct LineS {
   static constexpr bool kHist = true;
   __device__ __forceinline__ bool hist_rank(unsigned hint, int rho, unsigned* hist, unsigned* P, int* le,
                                             int* less, unsigned* hbase) const {
-#ifndef ACOSS_HIST_PV
     if constexpr (kWin) {
       if (win) {
         *hbase = base8;
         return hist_rank_w8(w8, base8, rho, hist, P, le, less);
       }
     }
-#endif
     const int lane = threadIdx.x & 63;
     const unsigned base = hint > 64u ? hint - 64u : 0u;
     *hbase = base;
@@ -971,7 +884,6 @@ struct LineS {
 // word 2q + half is the low / high half of the ballot of bit q. Lanes past 2 KQ get 0.
 template <int KQ>
 __device__ __forceinline__ uint32_t lane_words(uint32_t mask) {
-#ifndef ACOSS_LW_SELECT
   // each ballot half is wave-uniform (an SGPR): one v_writelane_b32 places it on its lane
   uint32_t out = 0;
 #pragma unroll
@@ -981,17 +893,6 @@ __device__ __forceinline__ uint32_t lane_words(uint32_t mask) {
     out = (uint32_t)acoss_writelane((int)(uint32_t)(bal >> 32), 2 * q + 1, (int)out);
   }
   return out;
-#else
-  const int lane = threadIdx.x & 63;
-  uint32_t out = 0;
-#pragma unroll
-  for (int q = 0; q < KQ; ++q) {
-    const unsigned long long bal = __ballot((mask >> LineS<KQ>::bit_of_q(q)) & 1u);
-    const uint32_t w = (lane & 1) ? (uint32_t)(bal >> 32) : (uint32_t)bal;
-    out = (lane >> 1) == q ? w : out;
-  }
-  return out;
-#endif
 }
 
 // Lines of 2049..4096 codes: two long-line halves held by one wave, elements [0, 2048) in A
@@ -1064,35 +965,6 @@ __device__ __forceinline__ unsigned prefix_of_rank(const LT& L, int rho, unsigne
   // unrolled SWAR body once): 0 hint, 1 gallop down, 2 gallop up, 3 bisect
   int mode = (hint != kNoHint) ? 0 : 3;
   unsigned step = 1;
-#ifdef ACOSS_SEARCH_BRANCHY
-  while (a < b) {
-    unsigned t;
-    if (mode == 0)
-      t = hint < a ? a : (hint > b ? b : hint);
-    else if (mode == 1)
-      t = (b - a > step) ? b - step : a;
-    else if (mode == 2)
-      t = (b - a > step) ? a + step - 1 : (a + b) >> 1;
-    else
-      t = (a + b) >> 1;
-    const int c = L.count_le(t);
-    ++*passes;
-    const bool greater = c > rho;
-    if (greater) {
-      b = t;
-      c_b = c;
-    } else {
-      a = t + 1;
-      c_am1 = c;
-    }
-    if (mode == 0)
-      mode = greater ? 1 : 2;
-    else if (mode == 1)
-      mode = greater ? (step <<= 1, 1) : 3;
-    else if (mode == 2)
-      mode = greater ? 3 : (step <<= 1, 2);
-  }
-#else
   // The same search with its control kept in integer arithmetic on wave-uniform values (the
   // compare result as a 0/1 int from the sign of rho - c, the mode transitions and step doublings
   // as 2-bit / 1-bit table lookups): no per-pass branches and no bool round trip through a VGPR.
@@ -1117,7 +989,6 @@ __device__ __forceinline__ unsigned prefix_of_rank(const LT& L, int rho, unsigne
     step <<= (kDouble >> idx) & 1u;
     mode = (int)((kNext >> (2u * idx)) & 3u);
   }
-#endif
   *le_out = c_b;
   *less_out = c_am1;
   return a;
@@ -1218,8 +1089,6 @@ __device__ __forceinline__ Group group_keys(const LT& L, unsigned P, int g, cons
     W.gv[t] = cell_gram(keyf.V, (keyf.qi(e) + u) * keyf.V.tau, (keyf.rj(e) + u) * keyf.V.tau);
   }
   __builtin_amdgcn_wave_barrier();
-  ACOSS_COUNT(KF::kRow ? 8 : 13, 1);
-  ACOSS_COUNT(KF::kRow ? 9 : 14, g);
   Group G;
   G.P = P;
   G.g = g;
@@ -1271,8 +1140,6 @@ __device__ __forceinline__ void group_keys2(const LT& L, unsigned P1, int g1, un
     W.gv[t] = cell_gram(keyf.V, (keyf.qi(e) + u) * keyf.V.tau, (keyf.rj(e) + u) * keyf.V.tau);
   }
   __builtin_amdgcn_wave_barrier();
-  ACOSS_COUNT(KF::kRow ? 8 : 13, 1);
-  ACOSS_COUNT(KF::kRow ? 9 : 14, g);
   unsigned key = 0xffffffffu;
   if (lane < g) {
     float dot = W.gv[lane * kMS];
@@ -1323,9 +1190,6 @@ __device__ __forceinline__ unsigned sort16_lanes(unsigned v) {
 
 // Key of rank rho (0-based) inside a batched group whose members start at lane 0 (off == 0).
 __device__ __forceinline__ unsigned group_rank(const Group& G, int rho) {
-#ifdef ACOSS_RANK_SORT16
-  if (G.g >= 6 && G.g <= 16) return (unsigned)__builtin_amdgcn_readlane((int)sort16_lanes(G.key), rho);
-#endif
   const int lane = threadIdx.x & 63;
   int cl = 0, ce = 0;
   for (int k = 0; k < G.g; ++k) {
@@ -1340,14 +1204,6 @@ __device__ __forceinline__ unsigned group_rank(const Group& G, int rho) {
 
 // Keys of ranks rho and rho + 1 inside a batched group (rho + 1 < g), one counting loop.
 __device__ __forceinline__ void group_rank2(const Group& G, int rho, unsigned* v0, unsigned* v1) {
-#ifdef ACOSS_RANK_SORT16
-  if (G.g >= 6 && G.g <= 16) {
-    const unsigned srt = sort16_lanes(G.key);
-    *v0 = (unsigned)__builtin_amdgcn_readlane((int)srt, rho);
-    *v1 = (unsigned)__builtin_amdgcn_readlane((int)srt, rho + 1);
-    return;
-  }
-#endif
   const int lane = threadIdx.x & 63;
   int cl = 0, ce = 0;
   for (int k = 0; k < G.g; ++k) {
@@ -1476,39 +1332,12 @@ __device__ __forceinline__ Plan line_plan(const LT& L, int n, float kappa, WaveL
   if (!hinted) L.min_max(&kmin, &kmax);
   int le = 0, less = 0;
   int passes = 0;
-  ACOSS_STAMP(ts0);
-#ifdef ACOSS_ABL_SEARCH2X  // timing ablation only: the search runs twice (same answer)
-  {
-    unsigned h2 = hint->P, a2 = kmin;
-    asm volatile("" : "+s"(h2), "+s"(a2));
-    int le2, less2, p2 = 0;
-    const unsigned P2 = prefix_of_rank(L, lo, a2, kmax, n, h2, &le2, &less2, &p2);
-    asm volatile("" ::"s"(P2), "s"(le2), "s"(less2));
-  }
-#endif
   unsigned Pl = 0u, hbase = 0u;
   bool found = false;
-#ifndef ACOSS_NO_HIST_SEARCH
   if constexpr (LT::kHist) {
     if (hinted) found = L.hist_rank(hint->P, lo, W.hist, &Pl, &le, &less, &hbase);
   }
-#endif
   if (!found) Pl = prefix_of_rank(L, lo, kmin, kmax, n, hint->P, &le, &less, &passes);
-  ACOSS_STAMP(ts1);
-  ACOSS_STAMP_ADD(KF::kRow ? 36 : 32, ts0, ts1);  // prefix search
-  ACOSS_COUNT(KF::kRow ? 6 : 11, 1);
-  ACOSS_COUNT(KF::kRow ? 7 : 12, passes);
-  if (!hinted) {
-    ACOSS_COUNT(KF::kRow ? 16 : 18, 1);
-    ACOSS_COUNT(KF::kRow ? 17 : 19, passes);
-  }
-#ifdef ACOSS_STAMPS
-  if (hinted) {
-    const unsigned dlt = Pl > hint->P ? Pl - hint->P : hint->P - Pl;
-    const int bin = dlt == 0 ? 0 : dlt == 1 ? 1 : dlt == 2 ? 2 : dlt <= 4 ? 3 : dlt <= 8 ? 4 : dlt <= 16 ? 5 : dlt <= 32 ? 6 : 7;
-    ACOSS_COUNT(20 + bin, 1);
-  }
-#endif
   hint->P = Pl;
   // density around the answer: the group at Pl, smoothed over the run
   hint->dens = hinted ? 0.5f * hint->dens + 0.5f * (float)(le - less) : (float)(le - less);
@@ -1522,11 +1351,7 @@ __device__ __forceinline__ Plan line_plan(const LT& L, int n, float kappa, WaveL
   // the upper statistic is the least key above Pl: its group from the histogram's bins, read now
   // (the bins belong to this line only until the next line's search)
   pl.next_ok = hi != lo && hi >= le && found && hist_next(W.hist, hbase, Pl, &pl.Ph2, &pl.gh2);
-#if !defined(ACOSS_NO_GROUP2) && !defined(ACOSS_ABL_NOGROUP) && !defined(ACOSS_ABL_NOGROUP2)
   pl.both = pl.next_ok && le - less <= 64 && (le - less) + pl.gh2 <= 64;
-#else
-  pl.both = false;
-#endif
   return pl;
 }
 
@@ -1538,12 +1363,6 @@ __device__ __forceinline__ void line_groups(const LT& L, const Plan& pl, const K
   const unsigned Pl = pl.Pl;
   const int le = pl.le, less = pl.less, lo = pl.lo, hi = pl.hi;
   unsigned vlo, vhi;
-  ACOSS_STAMP(ts1);
-#if defined(ACOSS_ABL_NOGROUP) || defined(ACOSS_ABL_NOGROUP2)
-  if (true) {
-    vlo = vhi = Pl << 16;
-  } else
-#endif
   if (pl.both) {
     group_keys2(L, Pl, le - less, pl.Ph2, pl.gh2, keyf, W, c_lo, c_hi);
     vlo = group_rank(*c_lo, lo - less);
@@ -1572,8 +1391,6 @@ __device__ __forceinline__ void line_groups(const LT& L, const Plan& pl, const K
       vhi = rank_in_prefix(L, Ph, 0, gh, keyf, W, c_hi);
     }
   }
-  ACOSS_STAMP(ts2);
-  ACOSS_STAMP_ADD(KF::kRow ? 37 : 33, ts1, ts2);  // group keys and ranks
   *vlo_o = vlo;
   *vhi_o = vhi;
 }
@@ -1615,9 +1432,6 @@ __device__ __forceinline__ auto le_bits(const LT& L, unsigned Tbits, const KF& k
   const unsigned T16 = Tbits >> 16;
   const int lane = threadIdx.x & 63;
   const auto word = L.le_mask(T16);  // kNone is never <= T16 <= 0x7f80
-#ifdef ACOSS_ABL_NOGROUP2  // timing ablation only (wrong results): prefix-only decision
-  return word;
-#endif
   // (selected by value: a pointer to either cached group would put both on the stack)
   const bool lo_hit = c_lo.g >= 0 && c_lo.P == T16, hi_hit = c_hi.g >= 0 && c_hi.P == T16;
   W.words[lane] = 0xffffffffu;
@@ -1632,7 +1446,6 @@ __device__ __forceinline__ auto le_bits(const LT& L, unsigned Tbits, const KF& k
     const int g = wave_sum(popc(L.eq_mask(T16)));
     if (g == 0) return word;
     if (g <= 64) {
-      ACOSS_COUNT(KF::kRow ? 10 : 15, 1);
       const Group G = group_keys(L, T16, g, keyf, W);
       if (lane < G.g && G.key > Tbits) atomicAnd(&W.words[LT::lane_of(G.elem)], ~(1u << LT::bit_of(G.elem)));
     } else {  // large group: member keys in rounds of 64
@@ -1721,25 +1534,17 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
     }
   };
   // Line2 loads each line when it starts (no prefetch: 48 VGPRs, the 4th wave per SIMD)
-#ifdef ACOSS_ROWS_NOPF  // no next-row prefetch (fewer VGPRs: occupancy over latency), for A/B
-  constexpr bool kPF = false;
-#else
   constexpr bool kPF = KQ != 2;
-#endif
   // one row's select on its loaded line L; prefetch() requests the wave's next line once this
   // one's window is built
   auto row = [&](LT& L, int r, auto&& prefetch) {
     const int i = i0 + r;
     uint64_t word = 0;  // (Line2: the second half's word in bits 32..63)
     if (i < V.Mp) {
-#ifndef ACOSS_NO_WINDOW8
-#ifndef ACOSS_NO_SAMPLE_HINT
       if (hint.P == kNoHint) hint.P = sample_hint(L, V.Np, kappa);
-#endif
       if constexpr (KQ != 8) {
         if (hint.P != kNoHint) L.build_window(hint.P);
       }
-#endif
       prefetch();
       const LineCells<true> keyf{V, i};
       float th, T;
@@ -1750,10 +1555,8 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
         thr[(size_t)p * thr_stride + i] = th;
         Tq[(size_t)p * thr_stride + i] = T;
       }
-#ifndef ACOSS_ABL_NOLEBITS
       word = le_bits(L, __builtin_bit_cast(unsigned, T), keyf, W, c_lo, c_hi);
       if constexpr (KQ == 8 || KQ == 16) word = lane_words<KQ>((uint32_t)word);  // lane t: columns 32t .. 32t + 31
-#endif
     }
     rowbits[r][lane] = (uint32_t)word;
     if constexpr (KQ == 2) rowbits[r][64 + lane] = (uint32_t)(word >> 32);
@@ -1783,9 +1586,6 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
   // the 32 x 32 bit block of columns 32b..32b+31 and transposes it in registers (five
   // masked-swap stages, about half an op per bit).
   uint32_t* out = RT + (size_t)p * rt_stride + (size_t)strip * ld;
-#ifdef ACOSS_ABL_NOTRANSPOSE
-  return;
-#endif
   for (int b = threadIdx.x; 32 * b < V.Np; b += NW * 64) {
     uint32_t a[32];
 #pragma unroll
@@ -1810,11 +1610,9 @@ __device__ __forceinline__ void rows_body(const PairView& V, int p, int strip, c
 // KQ = 8: every line of the launch is short; KQ = 0: each pair picks its row line type (rows of
 // at most short_n codes take LineS<8>; short_n = 0 disables); KQ = 16: as 0 with LineS<16> for
 // the rest (every line <= 1024 codes); KQ = 2: as 0, and rows past 2048 codes take Line2.
-#ifndef ACOSS_SWEEP_WPE
-#define ACOSS_SWEEP_WPE 4
-#endif
+constexpr int kSweepWPE = 4;  // sweep blocks per CU (waves per SIMD)
 // Arguments of one sweep + row-select launch (k_sweep_rows9) and of one column-select launch
-// (k_sel_cols9); the fused launch (k_sweep_cols9) takes one of each.
+// (k_sel_cols9).
 struct SweepArgs {
   CrpBatch B;
   KeyPlanes K;
@@ -1845,10 +1643,9 @@ struct ColsArgs {
 template <int KQ>
 constexpr int kSweepLds = KQ == 2 ? kRowsLds2 : kRowsLds;
 
-// One (32-row strip, pair) block of the sweep and its fused row select; smem: kSweepLds<KQ> bytes
-// plus one int (the ring slot).
+// One (32-row strip, pair) block of the sweep and its fused row select; smem: kSweepLds<KQ> bytes.
 template <int KQ>
-__device__ __forceinline__ void sweep_rows_block(const SweepArgs& A, int strip, int p, char* smem, int* s_slot_p) {
+__device__ __forceinline__ void sweep_rows_block(const SweepArgs& A, int strip, int p, char* smem) {
   constexpr int RB = KQ == 2 ? 128 : 64;  // row-bit words per row
   const CrpBatch& B = A.B;
   const KeyPlanes& K = A.K;
@@ -1861,35 +1658,12 @@ __device__ __forceinline__ void sweep_rows_block(const SweepArgs& A, int strip, 
   const PairView V = pair_view(B, p);
   const int i0 = strip * kSR;
   if (i0 >= V.Mp || V.Np <= 0) return;
-  // the strip's row-major plane: per pair, or a slot of this XCD's ring (HrRing)
-  int& s_slot = *s_slot_p;
   uint16_t* Hr = K.hr + (size_t)p * kstride + (size_t)i0 * ldr;
-  if (K.ring.slots) {
-    if (threadIdx.x == 0) {
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-      const unsigned long long t = atomicAdd(K.ring.ticket + 16 * xcc, 1ull);
-      const unsigned S = (unsigned)K.ring.slots;
-      const int slot = (int)(xcc * S + (unsigned)(t & (S - 1)));
-      const unsigned g = (unsigned)(t / S);
-      // the previous owner (ticket t - S of this XCD) started earlier and is resident or done;
-      // the acquire also invalidates this CU's L1 (stale lines of an earlier owner here)
-      while (__hip_atomic_load(K.ring.gen + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != g)
-        __builtin_amdgcn_s_sleep(2);
-      s_slot = slot;
-    }
-    __syncthreads();
-    Hr = K.ring.base + (size_t)__builtin_amdgcn_readfirstlane(s_slot) * kSR * ldr;  // wave-uniform (SGPR)
-  }
   if (i0 + kSR <= V.Mp)
     sweep_body_sys<false>(V, p, strip, K, ldr, ldc, kstride, Hr);
   else
     sweep_body_sys<true>(V, p, strip, K, ldr, ldc, kstride, Hr);
-  ACOSS_STAMP(r0);
   __syncthreads();  // the strip's F rows are complete (block-scope visibility of the global stores)
-#ifdef ACOSS_ABL_NOROWS  // timing ablation only (wrong results): sweep without the row select
-  return;
-#endif
   WaveLds* wl = reinterpret_cast<WaveLds*>(smem);
   uint32_t(*rowbits)[RB] = reinterpret_cast<uint32_t(*)[RB]>(smem + 4 * sizeof(WaveLds));
   // lines of <= short_n codes take LineS<8> in every launch type but KQ = 8 (all short); KQ = 16
@@ -1903,28 +1677,12 @@ __device__ __forceinline__ void sweep_rows_block(const SweepArgs& A, int strip, 
     rows_body<4, 2, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
   else
     rows_body<4, 0, RB>(V, p, strip, Hr, ldr, kappa, thr, Tq, thr_stride, RT, rt_stride, ld, wl, rowbits);
-  if (K.ring.slots) {  // every wave's reads of the slot have returned: hand it to ticket t + S
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(K.ring.gen + s_slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  ACOSS_STAMP(r1);
-  ACOSS_STAMP_ADD(4, r0, r1);  // row select
-  if (threadIdx.x == 0) ACOSS_STAMP_ADD(5, 0ull, 1ull);
 }
 
 template <int KQ>
-__global__ __launch_bounds__(kThreads, ACOSS_SWEEP_WPE) void k_sweep_rows9(SweepArgs A) {
+__global__ __launch_bounds__(kThreads, kSweepWPE) void k_sweep_rows9(SweepArgs A) {
   __shared__ __attribute__((aligned(16))) char smem[kSweepLds<KQ>];
-  __shared__ int s_slot;
-#ifdef ACOSS_SWEEP_XCD
-  // all strips of a pair on one XCD (its L2 then holds the pair's frames for the walk and for the
-  // row select's exact-key recompute)
-  const int nblk = gridDim.x * gridDim.y;
-  const int lb = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, nblk);
-  sweep_rows_block<KQ>(A, lb % gridDim.x, lb / gridDim.x, smem, &s_slot);
-#else
-  sweep_rows_block<KQ>(A, blockIdx.x, blockIdx.y, smem, &s_slot);
-#endif
+  sweep_rows_block<KQ>(A, blockIdx.x, blockIdx.y, smem);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1933,18 +1691,12 @@ __global__ __launch_bounds__(kThreads, ACOSS_SWEEP_WPE) void k_sweep_rows9(Sweep
 // stacked frames, so each column's search starts from the previous column's answer (the first
 // column of a run bisects from its min/max).
 // ---------------------------------------------------------------------------------------
-#ifndef ACOSS_CPW
-#define ACOSS_CPW 2
-#endif
+constexpr int kCPWLong = 2;  // columns per wave, long lines
 // short lines: a run start (sample guess, longer search) is a larger share of a cheap line
-#ifndef ACOSS_CPW_SHORT
-#define ACOSS_CPW_SHORT 4
-#endif
+constexpr int kCPWShort = 4;
 template <int KQ>
-constexpr int kCPW = (KQ == 8 || KQ == 16) ? ACOSS_CPW_SHORT : ACOSS_CPW;
-#ifndef ACOSS_COLS_WPE
-#define ACOSS_COLS_WPE 4
-#endif
+constexpr int kCPW = (KQ == 8 || KQ == 16) ? kCPWShort : kCPWLong;
+constexpr int kColsWPE = 4;  // column-select waves per SIMD
 template <int KQ>
 constexpr int kColsPerBlock = 4 * kCPW<KQ>;
 
@@ -1960,11 +1712,7 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
   Hint hint{kNoHint, 1.0f};
   // the next column's line is loaded while this one is searched (its HBM latency hidden)
   auto load_col = [&](LT& Ld, int j) {
-#ifdef ACOSS_ABL_HCRING
-    int64_t coloff = (int64_t)(p % ACOSS_ABL_HCRING) * kstride + (int64_t)j * kSR;
-#else
     int64_t coloff = (int64_t)p * kstride + (int64_t)j * kSR;
-#endif
     asm volatile("" : "+s"(coloff));  // per-column address: nothing per lane hoisted out of the loop
     if constexpr (KQ == 0) {
       Ld.template load_lanes<true>(K.hc + coloff, (size_t)ldc * kSR, V.Mp);
@@ -1978,15 +1726,10 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
   };
   // one column's select on its loaded line L
   auto column = [&](LT& L, int j) {
-#ifndef ACOSS_NO_WINDOW8
-#ifndef ACOSS_NO_SAMPLE_HINT
     if (hint.P == kNoHint) hint.P = sample_hint(L, V.Mp, kappa);
-#endif
     if constexpr (KQ != 8) {
       if (hint.P != kNoHint) L.build_window(hint.P);
     }
-#endif
-    ACOSS_COUNT(31, 1);  // columns
     // this column's row-threshold word, requested now and used after the select
     const size_t w = (size_t)p * mask_stride + (size_t)(lane * KPL < V.Mp ? lane : 0) * ld + j;
     const uint32_t rt = RT[w];
@@ -2002,26 +1745,11 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
       thr[(size_t)p * thr_stride + j] = th;
       Tq[(size_t)p * thr_stride + j] = Tc;
     }
-    ACOSS_STAMP(tc0);
-#ifdef ACOSS_ABL_NOLEBITS
-    const uint64_t bits = 0;
-#else
     uint64_t bits = le_bits(L, __builtin_bit_cast(unsigned, Tc), keyf, W, c_lo, c_hi);
     if constexpr (KQ == 8 || KQ == 16) bits = lane_words<KQ>((uint32_t)bits);  // lane s: rows 32s .. 32s + 31
-#endif
     if (lane * KPL < V.Mp) maskT[w] = (uint32_t)bits & rt;
     if (KQ == 2 && 2048 + lane * KPL < V.Mp) maskT[w2] = (uint32_t)(bits >> 32) & rt2;
-    ACOSS_STAMP(tc1);
-    ACOSS_STAMP_ADD(35, tc0, tc1);  // le_bits and the CRP word
   };
-#ifdef ACOSS_COLS_NOPF  // no next-column prefetch: 16 VGPRs fewer (occupancy over latency)
-#pragma unroll 1
-  for (int j = j0; j < jend; ++j) {
-    LT L;
-    load_col(L, j);
-    column(L, j);
-  }
-#else
   constexpr bool kPF = KQ != 2;  // as the rows
   // (both columns of a long-line pair in their own registers, fully unrolled, instead of the
   // copy of the prefetched line: -4.5 % at 2,000 frames, profiles/r04/ab_unroll2000.txt)
@@ -2039,7 +1767,6 @@ __device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int 
       column(L, j);
     }
   }
-#endif
 }
 
 
@@ -2077,35 +1804,9 @@ __device__ __forceinline__ void cols_block(const ColsArgs& A, int lin, int ncb, 
 }
 
 template <int KQ>
-__global__ __launch_bounds__(256, ACOSS_COLS_WPE) void k_sel_cols9(ColsArgs A) {
+__global__ __launch_bounds__(256, kColsWPE) void k_sel_cols9(ColsArgs A) {
   __shared__ WaveLds wl[4];
   cols_block<KQ>(A, blockIdx.y * gridDim.x + blockIdx.x, gridDim.x, gridDim.x * gridDim.y, wl);
-}
-
-// Fused launch: the sweep + row select of one sub-batch (nS blocks) and the column select of the
-// previous one (nC blocks) in ONE grid, so every CU holds a mix of the store-heavy walks and the
-// VALU-heavy selects instead of whatever one kernel leaves free for the other. Blocks come in
-// groups of 8 of one kind (8 consecutive blocks land on the 8 XCDs, so a select block's linear
-// index stays congruent to its XCD for xcd_remap), the kinds interleaved in proportion to their
-// group counts (Bresenham), so both progress together through the launch.
-template <int KQ>
-__global__ __launch_bounds__(kThreads, ACOSS_SWEEP_WPE) void k_sweep_cols9(SweepArgs S, int nstrips, int nS,
-                                                                           ColsArgs C, int ncb, int nC, int order) {
-  __shared__ __attribute__((aligned(16))) char smem[kSweepLds<KQ> > (int)(4 * sizeof(WaveLds)) ? kSweepLds<KQ>
-                                                                                               : (int)(4 * sizeof(WaveLds))];
-  __shared__ int s_slot;
-  const int gS = (nS + 7) >> 3, gC = (nC + 7) >> 3, gT = gS + gC;
-  const int b = blockIdx.x, g = b >> 3, x = b & 7;
-  // order 0: interleaved in proportion; 1: the select groups first; 2: the sweep groups first
-  const int s0 = order == 0 ? (int)(((int64_t)g * gS) / gT) : order == 1 ? max(0, g - gC) : min(g, gS);
-  const int s1 = order == 0 ? (int)(((int64_t)(g + 1) * gS) / gT) : order == 1 ? max(0, g + 1 - gC) : min(g + 1, gS);
-  if (s1 > s0) {  // a sweep group
-    const int v = 8 * s0 + x;
-    if (v < nS) sweep_rows_block<KQ>(S, v % nstrips, v / nstrips, smem, &s_slot);
-  } else {
-    const int c = 8 * (g - s0) + x;
-    if (c < nC) cols_block<KQ>(C, c, ncb, nC, reinterpret_cast<WaveLds*>(smem));
-  }
 }
 
 }  // namespace
@@ -2122,11 +1823,11 @@ static int split_kq(int L, int* short_n) {
   return L > 2048 ? 2 : (no_short ? 0 : (L <= 512 ? 8 : (L <= 1024 ? 16 : 0)));
 }
 
-static SweepArgs sweep_args(const CrpBatch& B, void* kplanes, const HrRing& ring, int ldk, int64_t kstride, int nb,
+static SweepArgs sweep_args(const CrpBatch& B, void* kplanes, int ldk, int64_t kstride, int nb,
                             float kappa, float* thr_r, float* T_r, int64_t thr_stride, uint32_t* RT,
                             int64_t mask_stride, int ld, int short_n) {
   const size_t plane = (size_t)nb * kstride;
-  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane, ring};
+  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane};
   return SweepArgs{B, K, ldk, ldk, kstride, kappa, thr_r, T_r, thr_stride, RT, mask_stride, ld, short_n};
 }
 
@@ -2134,14 +1835,14 @@ static ColsArgs cols_args(const CrpBatch& B, void* kplanes, int ldk, int64_t kst
                           const uint32_t* RT, float* thr_c, float* T_c, int64_t thr_stride, uint32_t* maskT,
                           int64_t mask_stride, int ld, int short_n) {
   const size_t plane = (size_t)nb * kstride;
-  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane, HrRing{}};
+  const KeyPlanes K{static_cast<uint16_t*>(kplanes), static_cast<uint16_t*>(kplanes) + plane};
   return ColsArgs{B, K, ldk, kstride, kappa, RT, thr_c, T_c, thr_stride, maskT, mask_stride, ld, short_n};
 }
 
 // Two-kernel CRP (m = 9, tau = 1, lines up to 4096 keys). Returns 1 if not applicable.
 // kplanes: nb * kstride uint16 row-major prefixes, then nb * kstride uint16 strip-major ones;
 // RT: nb * mask_stride words (same layout as maskT).
-int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, const HrRing& ring, int ldk,
+int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplanes, int ldk,
                      int64_t kstride,
                      uint32_t* RT, float* thr_r, float* T_r, float* thr_c, float* T_c, int64_t thr_stride,
                      uint32_t* maskT, int64_t mask_stride, int ld, hipStream_t s) {
@@ -2149,7 +1850,7 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
   const int nstrips = (L + kSR - 1) / kSR;
   int short_n;
   const int kq = split_kq(L, &short_n);
-  const SweepArgs SA = sweep_args(B, kplanes, ring, ldk, kstride, nb, kappa, thr_r, T_r, thr_stride, RT, mask_stride,
+  const SweepArgs SA = sweep_args(B, kplanes, ldk, kstride, nb, kappa, thr_r, T_r, thr_stride, RT, mask_stride,
                                   ld, short_n);
   const ColsArgs CA = cols_args(B, kplanes, ldk, kstride, nb, kappa, RT, thr_c, T_c, thr_stride, maskT, mask_stride,
                                 ld, short_n);
@@ -2171,46 +1872,5 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
   return launch(std::integral_constant<int, 0>{});
 }
 
-// One fused launch (k_sweep_cols9): the sweep + row select of sub-batch S (ns pairs, key planes
-// kpl_s, row words RT_s) and the column select of the previous sub-batch C (nc pairs, its planes
-// kpl_c and words RT_c, which an earlier launch on the same stream completed). Either may be empty.
-int launch_crp_split_fused(const SplitSide& S, const SplitSide& C, int L, float kappa, int ldk, int64_t kstride,
-                           int64_t thr_stride, int64_t mask_stride, int ld, hipStream_t s) {
-  if (S.B.m != kMS || S.B.tau != 1 || L > 4096) return 1;
-  const int nstrips = (L + kSR - 1) / kSR;
-  int short_n;
-  const int kq = split_kq(L, &short_n);
-  const SweepArgs SA = sweep_args(S.B, S.kpl, S.ring, ldk, kstride, S.nb > 0 ? S.nb : 1, kappa, S.thr_r, S.T_r,
-                                  thr_stride, S.RT, mask_stride, ld, short_n);
-  const ColsArgs CA = cols_args(C.B, C.kpl, ldk, kstride, C.nb > 0 ? C.nb : 1, kappa, C.RT, C.thr_c, C.T_c,
-                                thr_stride, C.maskT, mask_stride, ld, short_n);
-  auto launch = [&](auto kqc) -> int {
-    constexpr int KQ = decltype(kqc)::value;
-    const int ncb = (L + kColsPerBlock<KQ> - 1) / kColsPerBlock<KQ>;
-    const int nS = S.nb > 0 ? nstrips * S.nb : 0, nC = C.nb > 0 ? ncb * C.nb : 0;
-    const int blocks = 8 * (((nS + 7) >> 3) + ((nC + 7) >> 3));
-    if (blocks == 0) return ACOSS_OK;
-    const char* oenv = getenv("ACOSS_FUSED_ORDER");
-    const int order = oenv ? atoi(oenv) : 0;
-    hipLaunchKernelGGL(k_sweep_cols9<KQ>, dim3(blocks), dim3(kThreads), 0, s, SA, nstrips, nS, CA, ncb, nC, order);
-    ACOSS_LAUNCH_CHECK();
-    return ACOSS_OK;
-  };
-  if (kq == 8) return launch(std::integral_constant<int, 8>{});
-  if (kq == 16) return launch(std::integral_constant<int, 16>{});
-  if (kq == 2) return launch(std::integral_constant<int, 2>{});
-  return launch(std::integral_constant<int, 0>{});
-}
-
 }  // namespace acoss
 
-#ifdef ACOSS_STAMPS
-extern "C" int acoss_debug_sweep_stamps(unsigned long long* out16) {
-  if (hipDeviceSynchronize() != hipSuccess) return ACOSS_E_HIP;
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(acoss::d_sweep_stamps), 48 * sizeof(unsigned long long)) != hipSuccess)
-    return ACOSS_E_HIP;
-  unsigned long long z[48] = {};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(acoss::d_sweep_stamps), z, sizeof(z)) != hipSuccess) return ACOSS_E_HIP;
-  return ACOSS_OK;
-}
-#endif

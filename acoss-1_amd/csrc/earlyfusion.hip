@@ -423,20 +423,7 @@ __device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int
     }
     lo = wave_min_u32(mn);
     hi = wave_max_u32(mx);
-#ifdef ACOSS_EF_BISECT  // (the count-pass bisection, for A/B)
-    while (lo < hi) {
-      const unsigned mid = lo + ((hi - lo) >> 1);
-      int c = 0;
-#pragma unroll
-      for (int q = 0; q < KB; ++q) c += kr[q] <= mid;
-      if (wave_sum(c) >= nn)
-        hi = mid;
-      else
-        lo = mid + 1;
-    }
-#else
     lo = radix_kth(kr, lo, hi, nn, lane, hist);
-#endif
   } else {
     while (lo < hi) {
       const unsigned mid = lo + ((hi - lo) >> 1);

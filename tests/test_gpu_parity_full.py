@@ -74,12 +74,7 @@ def test_full_corpus_qmax_and_map_parity_500():
     {"ACOSS_KEY_BYTES": str(20 << 20)},                           # ~2 pairs per key-plane sub-batch
     {"ACOSS_SPLIT_STREAMS": "3", "ACOSS_KEY_BYTES": str(40 << 20)},
     {"ACOSS_BATCH_PAIRS": "5", "ACOSS_SPLIT_STREAMS": "1", "ACOSS_KEY_BYTES": "1"},  # 1 pair per sub-batch
-    {"ACOSS_SPLIT_FUSED": "0"},                                   # two streams of separate kernels
-    {"ACOSS_SPLIT_FUSED": "0", "ACOSS_KEY_BYTES": str(20 << 20)},
-    {"ACOSS_SPLIT_FUSED": "1"},                                   # fused launches (auto: lines > 1536 only)
-    {"ACOSS_SPLIT_FUSED": "1", "ACOSS_KEY_BYTES": str(20 << 20)},
-    {"ACOSS_SPLIT_FUSED": "1", "ACOSS_KEY_BYTES": "1"},           # fused launches of 1 + 1 pairs
-    {"ACOSS_SPLIT_FUSED": "1", "ACOSS_FUSED_ORDER": "1"},         # block order is free (A/B knob)
+    {"ACOSS_SPLIT_STREAMS": "2", "ACOSS_KEY_BYTES": "1"},         # 1-pair sub-batches on two streams
 ])
 def test_batching_branches_ragged(monkeypatch, env):
     from acoss.engine import ChromaBank
@@ -155,21 +150,3 @@ def test_eval_ranks_ties_inf_nan():
         assert (a == b) or (np.isnan(a) and np.isnan(b)), (a, b)
 
 
-@pytest.mark.parametrize("slots", ["0", "1", "4", "32", "128"])
-def test_hr_ring_slots(monkeypatch, slots):
-    """The row-major key plane as per-XCD rings of strip slots (ACOSS_HR_RING; 1 slot per XCD
-    serialises the sweep blocks of each XCD through one buffer) against the oracle, including
-    short (LineS) and long (Line2) lines in one launch."""
-    from acoss.engine import ChromaBank
-    monkeypatch.setenv("ACOSS_HR_RING", slots)
-    rng = np.random.default_rng(int(slots) + 3)
-    lens = list(rng.integers(60, 1300, size=9)) + [2300, 480]
-    tracks = [synthetic.render(rng, synthetic.base_sequence(rng, int(n))) for n in lens]
-    pairs = _all_pairs(len(tracks))
-    feats, off, ln = synthetic.pack(tracks)
-    oq, od, _ = oracle.crp_batch(feats, off, ln, pairs, dmax=True, nthreads=_threads())
-    bank = ChromaBank(tracks)
-    for _ in range(2):  # a second call reuses the rings (tickets keep counting)
-        out = bank.crp_align(pairs, qmax=True, dmax=True)
-        np.testing.assert_array_equal(out["qmax"].cpu().numpy(), oq)
-        np.testing.assert_array_equal(out["dmax"].cpu().numpy(), od)
