@@ -40,3 +40,30 @@ def test_world2_equals_world1_full_size(datacos_full, algo):
         assert d1[k][1] == str((15000, 15000)), d1[k]
         assert int(d1[k][2]) > 0
         assert d1[k][0] == d2[k][0], (k, d1[k], d2[k])
+
+
+@pytest.fixture(scope="module")
+def datacos_full_ef(tmp_path_factory):
+    root = tmp_path_factory.mktemp("dtfull_ef")
+    tracks, labels = synthetic.make_hard_corpus("datacos", frames=240, seed=20250101, fixed_length=False)
+    tracks, labels = tracks[:15000], np.asarray(labels[:15000], np.int32)
+    csv, fdir = synthetic.write_feature_dataset(str(root), tracks, labels, with_mfcc=True, beat_period=5,
+                                                chroma_keys=("hpcp",), mfcc_from_chroma=True)
+    return root, csv, fdir
+
+
+@pytest.mark.timeout(900)
+def test_earlyfusion_world2_equals_world1_full_size(datacos_full_ef):
+    """Config 5 through coverid.benchmark("EarlyFusionTraile") at the Da-TACOS track count on one and
+    on two gloo ranks: the four score matrices are all-gathered onto both ranks, the SNF late and
+    early+late fusions run on both (sharded by the measured rule), and all six 15,000 x 15,000
+    matrices have the world-1 SHA-256."""
+    root, csv, fdir = datacos_full_ef
+    env = {"ACOSS_MR_DIGEST": "1"}
+    d1 = _run("bench:EarlyFusionTraile", 1, root, csv, fdir, "full", env_extra=env, timeout=800)
+    d2 = _run("bench:EarlyFusionTraile", 2, root, csv, fdir, "full", env_extra=env, timeout=800)
+    assert set(d1) == set(d2) == {"mfccs", "ssms", "chromas", "early", "late", "early+late"}
+    for k in d1:
+        assert d1[k][1] == str((15000, 15000)), d1[k]
+        assert int(d1[k][2]) > 0
+        assert d1[k][0] == d2[k][0], (k, d1[k], d2[k])
