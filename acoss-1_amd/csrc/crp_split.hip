@@ -1662,35 +1662,25 @@ __global__ __launch_bounds__(kThreads, kSweepWPE) void k_sweep_rows9(SweepArgs A
 // stacked frames, so each column's search starts from the previous column's answer (the first
 // column of a run bisects from its min/max).
 // ---------------------------------------------------------------------------------------
-#ifdef ACOSS_HW_OFF
-constexpr int kCPWLong = 2;
-#else
-constexpr int kCPWLong = 4;  // columns per wave, long lines (two runs of kRunH, one per half-wave)
-#endif
+constexpr int kCPWLong = 2;  // columns per wave, long lines
 // short lines: a run start (sample guess, longer search) is a larger share of a cheap line
 constexpr int kCPWShort = 4;
 template <int KQ>
 constexpr int kCPW = (KQ == 8 || KQ == 16) ? kCPWShort : kCPWLong;
-#ifndef ACOSS_COLS_WPE
-#define ACOSS_COLS_WPE 4
-#endif
-constexpr int kColsWPE = ACOSS_COLS_WPE;  // column-select waves per SIMD
+constexpr int kColsWPE = 4;  // column-select waves per SIMD
 template <int KQ>
 constexpr int kColsPerBlock = 4 * kCPW<KQ>;
 
 // Columns [j0, jend) of pair p with line type LineOf<KQ>.
-// (hint0: the search hint of the run's first column, kNoHint for a sample guess; returns the last
-// column's answer prefix, the next column's hint)
 template <int KQ>
-__device__ __forceinline__ unsigned cols_body(const PairView& V, int p, int j0, int jend, const KeyPlanes& K, int ldc,
-                                              int64_t kstride, float kappa, const uint32_t* __restrict__ RT,
-                                              float* __restrict__ thr, float* __restrict__ Tq, int64_t thr_stride,
-                                              uint32_t* __restrict__ maskT, int64_t mask_stride, int ld, WaveLds& W,
-                                              unsigned hint0 = kNoHint) {
+__device__ __forceinline__ void cols_body(const PairView& V, int p, int j0, int jend, const KeyPlanes& K, int ldc,
+                                          int64_t kstride, float kappa, const uint32_t* __restrict__ RT,
+                                          float* __restrict__ thr, float* __restrict__ Tq, int64_t thr_stride,
+                                          uint32_t* __restrict__ maskT, int64_t mask_stride, int ld, WaveLds& W) {
   constexpr int KPL = 32;  // rows per CRP word (= per lane for long lines)
   using LT = typename LineOf<KQ>::T;
   const int lane = threadIdx.x & 63;
-  Hint hint{hint0, 1.0f};
+  Hint hint{kNoHint, 1.0f};
   // the next column's line is loaded while this one is searched (its HBM latency hidden)
   auto load_col = [&](LT& Ld, int j) {
     int64_t coloff = (int64_t)p * kstride + (int64_t)j * kSR;
@@ -1748,424 +1738,6 @@ __device__ __forceinline__ unsigned cols_body(const PairView& V, int p, int j0, 
       column(L, j);
     }
   }
-  return hint.P;
-}
-
-
-// ---------------------------------------------------------------------------------------
-// Half-wave long-line column select: TWO CRP columns per wave, one per 32-lane half (half h:
-// lanes 32 h .. 32 h + 31; lane hl = lane & 31). Lane hl of half h holds rows 64 hl .. 64 hl + 63
-// of its half's column as two Line<32>-layout sub-lines (s = 0, 1: the 64-B split-order chunk of
-// strip 2 hl + s in the strip-major plane). A per-element step costs the wave what it costs for
-// one full-wave line (64 codes per wave-instruction), but every per-line step -- the scan and
-// picks of the histogram rank, the exact-key recompute round, the ranks, the threshold arithmetic
-// -- serves both columns in one pass. A column the fast path cannot settle (answer outside the
-// 128-code window, the next group outside the histogram, more than 64 members in the four groups,
-// a threshold prefix outside the recomputed groups) is redone by the full-wave select
-// (cols_body<0>), which writes the same outputs: bit-identical either way.
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ int hw_half() { return (int)(threadIdx.x >> 5) & 1; }
-#ifdef ACOSS_HW_STATS
-__device__ unsigned long long d_hw_stats[8];
-#define HW_STAT(i, v) if ((threadIdx.x & 63) == 0) atomicAdd(&d_hw_stats[i], (unsigned long long)(v))
-#else
-#define HW_STAT(i, v)
-#endif
-
-// Inclusive scan within each 32-lane half (wave_incl_scan's first five steps).
-__device__ __forceinline__ unsigned half_incl_scan(unsigned v) {
-  v += dpp_u32<0x111>(0u, v);
-  v += dpp_u32<0x112>(0u, v);
-  v += dpp_u32<0x114>(0u, v);
-  v += dpp_u32<0x118>(0u, v);
-  v += dpp_u32<0x142, 0xa>(0u, v);
-  return v;
-}
-// lane s0 of half 0 and lane s1 of half 1 (s0, s1 in 0..31, wave-uniform)
-struct Pick2 {
-  unsigned v0, v1;
-  __device__ __forceinline__ unsigned own() const { return hw_half() ? v1 : v0; }
-};
-__device__ __forceinline__ Pick2 half_pick(unsigned x, int s0, int s1) {
-  return Pick2{(unsigned)__builtin_amdgcn_readlane((int)x, s0), (unsigned)__builtin_amdgcn_readlane((int)x, 32 + s1)};
-}
-__device__ __forceinline__ Pick2 half_min(unsigned v) {
-  const unsigned I = 0xffffffffu;
-  v = min(v, dpp_u32<0x111>(I, v));
-  v = min(v, dpp_u32<0x112>(I, v));
-  v = min(v, dpp_u32<0x114>(I, v));
-  v = min(v, dpp_u32<0x118>(I, v));
-  v = min(v, dpp_u32<0x142, 0xa>(I, v));
-  return half_pick(v, 31, 31);
-}
-__device__ __forceinline__ Pick2 half_max(unsigned v) {
-  v = max(v, dpp_u32<0x111>(0u, v));
-  v = max(v, dpp_u32<0x112>(0u, v));
-  v = max(v, dpp_u32<0x114>(0u, v));
-  v = max(v, dpp_u32<0x118>(0u, v));
-  v = max(v, dpp_u32<0x142, 0xa>(0u, v));
-  return half_pick(v, 31, 31);
-}
-__device__ __forceinline__ uint64_t low_mask64(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
-__device__ __forceinline__ int ctz_or0(uint64_t m) { return m ? __builtin_ctzll(m) : 0; }
-
-// LDS of one wave of the half-wave select (aliases the wave's WaveLds): group member list,
-// the two columns' le words, and the two histograms (128 bins + 32 lane-private sinks each),
-// later overwritten by the Gram terms of the recompute round and the members' keys.
-struct alignas(16) WaveLdsH {
-  int list[64];
-  uint32_t words[128];  // half h: words 64 h + 2 hl + s
-  union {
-    uint32_t hist[2][160];
-    float gv[64 * kMS];
-    unsigned keys[64];
-  };
-};
-static_assert(sizeof(WaveLdsH) <= sizeof(WaveLds), "the half-wave LDS must fit the wave's WaveLds");
-
-struct LineH {
-  unsigned pv[2][16];  // sub-line s: element 64 hl + 32 s + q; word k = q k (bits 0..15) and q k + 16
-  unsigned w8[2][8];   // 7-bit window codes (Line<32>::build_window's layout), base8 per half
-  unsigned base8;
-  // Sub-line s is the 64-B chunk of strip 2 hl + s at u16 address col0 + (2 hl + s) * sstride
-  // (col0: this half's column in the strip-major plane). Chunks past the line (32 (2 hl + s) >= n)
-  // read strip 0 and become kNone; inside the last chunk the plane holds kNone past the line.
-  __device__ __forceinline__ void load(const uint16_t* col0, size_t sstride, int n) {
-    const int hl = threadIdx.x & 31;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int st = 2 * hl + s;
-      const bool in = 32 * st < n;
-      const uint4* src = reinterpret_cast<const uint4*>(col0 + (in ? (size_t)st * sstride : (size_t)0));
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = src[q];
-        pv[s][4 * q + 0] = in ? v.x : kNone * 0x10001u;
-        pv[s][4 * q + 1] = in ? v.y : kNone * 0x10001u;
-        pv[s][4 * q + 2] = in ? v.z : kNone * 0x10001u;
-        pv[s][4 * q + 3] = in ? v.w : kNone * 0x10001u;
-      }
-    }
-  }
-  __device__ __forceinline__ void build_window(unsigned center) {
-    base8 = center > 63u ? center - 63u : 0u;
-    const unsigned B2 = base8 * 0x10001u;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      unsigned c[16];
-#pragma unroll
-      for (int h = 0; h < 16; ++h) c[h] = pk_min_u16(pk_subsat_u16(pv[s][h], B2), 0x007f007fu);
-#pragma unroll
-      for (int h = 0; h < 8; ++h) w8[s][h] = __builtin_amdgcn_perm(c[h + 8], c[h], 0x06020400u);
-    }
-  }
-  // bit 32 s + q: element 64 hl + 32 s + q has prefix P (P an exact code: base8 < P <= base8 + 126,
-  // or base8 == 0 and P <= 126)
-  __device__ __forceinline__ uint64_t eq_mask(unsigned P) const {
-    const unsigned PP = (P - base8) * 0x01010101u;
-    uint32_t ne[2] = {0u, 0u};
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int h = 0; h < 8; ++h) ne[s] = gather_flags8(ne[s], (w8[s][h] ^ PP) + 0x7f7f7f7fu, h);
-    return (uint64_t)~ne[0] | ((uint64_t)~ne[1] << 32);
-  }
-  // bit 32 s + q: prefix <= x, on the window codes (x <= base8 + 126) or the 16-bit words
-  __device__ __forceinline__ uint32_t le8(int s, unsigned x) const {
-    const unsigned X4 = (x - base8 + 0x80u) * 0x01010101u;
-    uint32_t m = 0;
-#pragma unroll
-    for (int h = 0; h < 8; ++h) m = gather_flags8(m, X4 - w8[s][h], h);
-    return m;
-  }
-  __device__ __forceinline__ uint32_t le16(int s, unsigned x) const {
-    const unsigned X2 = (x + 0x8000u) * 0x10001u;
-    uint32_t m = 0;
-#pragma unroll
-    for (int h = 0; h < 16; ++h) m = gather_flags(m, X2 - pv[s][h], h);
-    return m;
-  }
-};
-
-// Sample guess of both halves' lines (run starts): the quantile's order statistic among the
-// elements 64 hl and 64 hl + 32 of each half (up to 64 samples), by ballot bisection; the two
-// bisections run together (per-half bounds, wave-uniform).
-__device__ __forceinline__ Pick2 hw_sample_hint(const LineH& L, int n, float kappa) {
-  const unsigned a = L.pv[0][0] & 0xffffu, b = L.pv[1][0] & 0xffffu;
-  const uint64_t va = __ballot(a != kNone), vb = __ballot(b != kNone);
-  const int ns0 = __builtin_popcount((uint32_t)va) + __builtin_popcount((uint32_t)vb);
-  const int ns1 = __builtin_popcount((uint32_t)(va >> 32)) + __builtin_popcount((uint32_t)(vb >> 32));
-  const float f = (float)(n - 1) * kappa * __builtin_amdgcn_rcpf((float)n);
-  const int k0 = (int)(f * (float)ns0), k1 = (int)(f * (float)ns1);
-  const Pick2 mn = half_min(min(a, b));
-  const Pick2 mx = half_max(max(a != kNone ? a : 0u, b != kNone ? b : 0u));
-  unsigned lo0 = mn.v0, hi0 = mx.v0, lo1 = mn.v1, hi1 = mx.v1;
-#pragma unroll 1
-  while (lo0 < hi0 || lo1 < hi1) {
-    const unsigned m0 = (lo0 + hi0) >> 1, m1 = (lo1 + hi1) >> 1;
-    const unsigned mid = hw_half() ? m1 : m0;
-    const uint64_t ba = __ballot(a <= mid), bb = __ballot(b <= mid);
-    const int c0 = __builtin_popcount((uint32_t)ba) + __builtin_popcount((uint32_t)bb);
-    const int c1 = __builtin_popcount((uint32_t)(ba >> 32)) + __builtin_popcount((uint32_t)(bb >> 32));
-    if (lo0 < hi0) {
-      if (c0 > k0) hi0 = m0; else lo0 = m0 + 1;
-    }
-    if (lo1 < hi1) {
-      if (c1 > k1) hi1 = m1; else lo1 = m1 + 1;
-    }
-  }
-  return Pick2{lo0 > 0x7f80u ? 0x7f80u : lo0, lo1 > 0x7f80u ? 0x7f80u : lo1};
-}
-
-// One column per half through the fast path. ja / jb: the two halves' columns (jb == ja when
-// half 1 has no column of its own: its outputs are suppressed). hint: per-half window centres.
-// Returns per half (bit h of *ok) whether it settled its column, and the answer prefixes (the next
-// hints) in *ans.
-__device__ __forceinline__ void cols_pair_h(const PairView& V, int p, int ja, int jb, bool actb, LineH& L,
-                                            const Pick2& hint, float kappa, const uint32_t* __restrict__ RT,
-                                            float* __restrict__ thr, float* __restrict__ Tq, int64_t thr_stride,
-                                            uint32_t* __restrict__ maskT, int64_t mask_stride, int ld, WaveLdsH& W,
-                                            int* ok_out, Pick2* ans) {
-  const int lane = threadIdx.x & 63, hl = lane & 31, half = hw_half();
-  const int n = V.Mp;
-  const int jme = half ? jb : ja;
-  // this lane's two CRP words' row-threshold words, requested now and used at the end
-  const int st0 = 2 * hl, st1 = 2 * hl + 1;
-  const size_t w0 = (size_t)p * mask_stride + (size_t)(32 * st0 < n ? st0 : 0) * ld + jme;
-  const size_t w1 = (size_t)p * mask_stride + (size_t)(32 * st1 < n ? st1 : 0) * ld + jme;
-  const uint32_t rt0 = RT[w0], rt1 = RT[w1];
-  L.build_window(hint.own());
-  const float q = (float)(n - 1) * kappa;
-  const float lo_f = floorf(q), hi_f = ceilf(q);
-  const int lo = (int)lo_f, hi = (int)hi_f;
-
-  // ---- histogram rank of lo in each half's window ----
-  typedef __attribute__((address_space(3))) unsigned lds_u32;
-  unsigned* hist = W.hist[half];
-  reinterpret_cast<uint4*>(hist)[hl] = make_uint4(0u, 0u, 0u, 0u);
-  __builtin_amdgcn_wave_barrier();
-  {
-    const unsigned hb = (unsigned)(size_t)(lds_u32*)hist;
-    const unsigned sk = hb + 512u + 4u * (unsigned)hl;
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int h = 0; h < 8; ++h)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const unsigned c = (L.w8[s][h] >> (8 * k)) & 0xffu;
-          const unsigned a = c < 127u ? hb + 4u * c : sk;
-          __hip_atomic_fetch_add((lds_u32*)(size_t)a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        }
-  }
-  __builtin_amdgcn_wave_barrier();
-  const uint4 hv = reinterpret_cast<const uint4*>(hist)[hl];
-  const unsigned c0 = hv.x, c01 = c0 + hv.y, c012 = c01 + hv.z, sl = c012 + hv.w;
-  const unsigned S = half_incl_scan(sl), E = S - sl;
-  // if rank lo falls into this lane's bins: its bin, prefix and counts
-  const int r = lo - (int)E;
-  const unsigned bsel = (unsigned)(r >= (int)c0) + (unsigned)(r >= (int)c01) + (unsigned)(r >= (int)c012);
-  const unsigned below = bsel == 0 ? 0u : bsel == 1 ? c0 : bsel == 2 ? c01 : c012;
-  const unsigned inbin = bsel == 0 ? hv.x : bsel == 1 ? hv.y : bsel == 2 ? hv.z : hv.w;
-  const uint64_t bal = __ballot((int)E <= lo && lo < (int)S);
-  const int s0 = ctz_or0((uint32_t)bal), s1 = ctz_or0(bal >> 32);
-  const Pick2 Pl = half_pick(L.base8 + 4u * (unsigned)hl + bsel, s0, s1);
-  const Pick2 less = half_pick(E + below, s0, s1);
-  const Pick2 le = half_pick(E + below + inbin, s0, s1);
-  const Pick2 b8 = half_pick(L.base8, 0, 0);
-  const bool f0 = (uint32_t)bal != 0u && !(b8.v0 > 0u && Pl.v0 == b8.v0);
-  const bool f1 = (uint32_t)(bal >> 32) != 0u && !(b8.v1 > 0u && Pl.v1 == b8.v1);
-  // ---- the upper statistic's group when it is the next non-empty prefix ----
-  const bool nh0 = hi != lo && hi >= (int)le.v0, nh1 = hi != lo && hi >= (int)le.v1;
-  Pick2 Ph{0u, 0u}, gh{0u, 0u};
-  bool g0ok = true, g1ok = true;
-  if (nh0 || nh1) {
-    const unsigned P = Pl.own();
-    const unsigned b0 = L.base8 + 4u * (unsigned)hl;
-    const bool e0 = hv.x && b0 > P, e1 = hv.y && b0 + 1u > P, e2 = hv.z && b0 + 2u > P, e3 = hv.w && b0 + 3u > P;
-    const unsigned fb = e0 ? 0u : e1 ? 1u : e2 ? 2u : 3u;
-    const unsigned fc = e0 ? hv.x : e1 ? hv.y : e2 ? hv.z : hv.w;
-    const uint64_t bn = __ballot(e0 || e1 || e2 || e3);
-    const int t0 = ctz_or0((uint32_t)bn), t1 = ctz_or0(bn >> 32);
-    Ph = half_pick(b0 + fb, t0, t1);
-    gh = half_pick(fc, t0, t1);
-    g0ok = (uint32_t)bn != 0u;
-    g1ok = (uint32_t)(bn >> 32) != 0u;
-  }
-  const unsigned glo0 = le.v0 - less.v0, glo1 = le.v1 - less.v1;
-  const unsigned ghi0 = nh0 ? gh.v0 : 0u, ghi1 = nh1 ? gh.v1 : 0u;
-  bool ok0 = f0 && (!nh0 || g0ok), ok1 = f1 && (!nh1 || g1ok);
-  if ((ok0 ? glo0 + ghi0 : 0u) + (ok1 ? glo1 + ghi1 : 0u) > 64u) ok0 = ok1 = false;
-  if (!(ok0 || ok1)) {
-    *ok_out = 0;
-    *ans = Pl;
-    return;
-  }
-  // group boundaries in the member list [lo h0 | lo h1 | hi h0 | hi h1] (a failed half's empty)
-  const unsigned gl0 = ok0 ? glo0 : 0u, gl1 = ok1 ? glo1 : 0u, gu0 = ok0 ? ghi0 : 0u, gu1 = ok1 ? ghi1 : 0u;
-  const unsigned A1 = gl0, A2 = gl0 + gl1, A3 = A2 + gu0, GT = A3 + gu1;
-  __builtin_amdgcn_wave_barrier();  // the bins are read: the recompute round reuses their LDS
-
-  // ---- exact keys of the groups, one batched round ----
-  {
-    const bool okme = half ? ok1 : ok0;
-    uint64_t mlo = okme ? L.eq_mask(Pl.own()) : 0ull;
-    uint64_t mhi = (okme && (half ? nh1 : nh0)) ? L.eq_mask(Ph.own()) : 0ull;
-    const unsigned pk = (unsigned)__builtin_popcountll(mlo) | ((unsigned)__builtin_popcountll(mhi) << 16);
-    const unsigned sc = (unsigned)wave_incl_scan((int)pk) - pk;  // half 1's slots follow half 0's
-    unsigned ilo = sc & 0xffffu, ihi = A2 + (sc >> 16);
-    const int tag = half << 12, eb = 64 * hl;
-    while (mlo) {
-      W.list[ilo++] = tag | (eb + __builtin_ctzll(mlo));
-      mlo &= mlo - 1ull;
-    }
-    while (mhi) {
-      W.list[ihi++] = tag | (eb + __builtin_ctzll(mhi));
-      mhi &= mhi - 1ull;
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  // this lane's member (lanes >= GT take member 0: a valid cell) and its norms, requested before
-  // the Gram terms so that their latency overlaps them
-  const int ent = W.list[lane < (int)GT ? lane : 0];
-  const int e = ent & 0xfff;
-  const float nq_me = V.NXq[e], nr_me = V.NXr[(ent >> 12) ? jb : ja];
-  for (int t = lane; t < kMS * (int)GT; t += 64) {
-    const int k = t / kMS, u = t - k * kMS;
-    const int en = W.list[k];
-    W.gv[t] = cell_gram(V, (en & 0xfff) + u, ((en >> 12) ? jb : ja) + u);
-  }
-  __builtin_amdgcn_wave_barrier();
-  unsigned key = 0xffffffffu;
-  if (lane < (int)GT) {
-    float dot = W.gv[lane * kMS];
-#pragma unroll
-    for (int u = 1; u < kMS; ++u) dot = dot + W.gv[lane * kMS + u];
-    const float d2 = (nq_me - 2.0f * dot) + nr_me;
-    key = __builtin_bit_cast(unsigned, d2 > 0.0f ? d2 : 0.0f);
-  }
-  __builtin_amdgcn_wave_barrier();
-  W.keys[lane] = key;
-  __builtin_amdgcn_wave_barrier();
-  // ---- ranks inside the groups ----
-  const int gid = lane < (int)A1 ? 0 : lane < (int)A2 ? 1 : lane < (int)A3 ? 2 : 3;
-  const int gstart = gid == 0 ? 0 : gid == 1 ? (int)A1 : gid == 2 ? (int)A2 : (int)A3;
-  const int gsize = gid == 0 ? (int)gl0 : gid == 1 ? (int)gl1 : gid == 2 ? (int)gu0 : (int)gu1;
-  const int gmax = (int)max(max(gl0, gl1), max(gu0, gu1));
-  int cl = 0, ce = 0;
-  for (int k = 0; k < gmax; ++k) {
-    const unsigned o = W.keys[gstart + min(k, max(gsize - 1, 0))];
-    if (k < gsize) {
-      cl += o < key;
-      ce += o == key;
-    }
-  }
-  const bool mem = lane < (int)GT;
-  const int m_half = (gid & 1);
-  const int lessm = (int)(m_half ? less.v1 : less.v0);
-  const int lem = (int)(m_half ? le.v1 : le.v0);
-  const bool inlo = gid < 2;
-  const int tl = lo - lessm, th2 = hi - lessm;
-  const uint64_t blo = __ballot(mem && inlo && cl <= tl && tl < cl + ce);
-  const bool hi_in_lo = hi != lo && hi < lem;
-  const uint64_t bhi = __ballot(mem && ((inlo && hi_in_lo && cl <= th2 && th2 < cl + ce) || (!inlo && cl == 0)));
-  const uint64_t r0 = low_mask64((int)A1), r1 = low_mask64((int)A2) & ~r0, r2 = low_mask64((int)A3) & ~low_mask64((int)A2),
-                 r3 = low_mask64((int)GT) & ~low_mask64((int)A3);
-  const unsigned vlo0 = (unsigned)__builtin_amdgcn_readlane((int)key, ctz_or0(blo & r0));
-  const unsigned vlo1 = (unsigned)__builtin_amdgcn_readlane((int)key, ctz_or0(blo & r1));
-  const unsigned vhi0 = hi == lo ? vlo0 : (unsigned)__builtin_amdgcn_readlane((int)key, ctz_or0(bhi & (r0 | r2)));
-  const unsigned vhi1 = hi == lo ? vlo1 : (unsigned)__builtin_amdgcn_readlane((int)key, ctz_or0(bhi & (r1 | r3)));
-  // ---- thresholds (both halves' in one pass) ----
-  const float slo = sqrt_rn(__builtin_bit_cast(float, half ? vlo1 : vlo0));
-  float th;
-  if (lo_f == hi_f) {
-    th = slo;
-  } else {
-    const float shi = sqrt_rn(__builtin_bit_cast(float, half ? vhi1 : vhi0));
-    const float aa = slo * (hi_f - q);
-    const float bb = shi * (q - lo_f);
-    th = aa + bb;
-  }
-  const float Tf = sq_threshold(th);
-  const unsigned Tb = __builtin_bit_cast(unsigned, Tf), T16 = Tb >> 16;
-  const Pick2 T16p = half_pick(T16, 0, 0), Tbp = half_pick(Tb, 0, 0);
-  // the threshold's prefix must be a recomputed group's (or an empty prefix between them)
-  ok0 = ok0 && (T16p.v0 == Pl.v0 || (nh0 && Pl.v0 < T16p.v0 && T16p.v0 <= Ph.v0));
-  ok1 = ok1 && (T16p.v1 == Pl.v1 || (nh1 && Pl.v1 < T16p.v1 && T16p.v1 <= Ph.v1));
-  // ---- le words: prefix <= T16, minus the members of T16's group above T ----
-  const bool win = T16 <= L.base8 + 126u;
-  uint32_t lw0, lw1;
-  if (__ballot(!win)) {
-    lw0 = L.le16(0, T16);
-    lw1 = L.le16(1, T16);
-  } else {
-    lw0 = L.le8(0, T16);
-    lw1 = L.le8(1, T16);
-  }
-  W.words[64 * half + 2 * hl] = 0xffffffffu;
-  W.words[64 * half + 2 * hl + 1] = 0xffffffffu;
-  __builtin_amdgcn_wave_barrier();
-  if (mem) {
-    const unsigned gp = gid == 0 ? Pl.v0 : gid == 1 ? Pl.v1 : gid == 2 ? Ph.v0 : Ph.v1;
-    const unsigned t16 = m_half ? T16p.v1 : T16p.v0, tb = m_half ? Tbp.v1 : Tbp.v0;
-    if (gp == t16 && key > tb) atomicAnd(&W.words[64 * m_half + 2 * (e >> 6) + ((e >> 5) & 1)], ~(1u << (e & 31)));
-  }
-  __builtin_amdgcn_wave_barrier();
-  lw0 &= W.words[64 * half + 2 * hl];
-  lw1 &= W.words[64 * half + 2 * hl + 1];
-  const bool okme = half ? ok1 : ok0;
-  const bool act = okme && (half == 0 || actb);
-  if (act) {
-    if (32 * st0 < n) maskT[w0] = lw0 & rt0;
-    if (32 * st1 < n) maskT[w1] = lw1 & rt1;
-    if (hl == 0) {
-      thr[(size_t)p * thr_stride + jme] = th;
-      Tq[(size_t)p * thr_stride + jme] = Tf;
-    }
-  }
-  *ok_out = (ok0 ? 1 : 0) | (ok1 ? 2 : 0);
-  *ans = Pl;
-}
-
-// Columns [j0, jend) of pair p, two runs per wave: half 0 takes j0 .. j0 + kRunH - 1, half 1
-// j0 + kRunH .. j0 + 2 kRunH - 1; each run starts from a sample guess and then chains its answers.
-constexpr int kRunH = 2;
-__device__ __forceinline__ void cols_body_h(const PairView& V, int p, int j0, int jend, const KeyPlanes& K, int ldc,
-                                            int64_t kstride, float kappa, const uint32_t* __restrict__ RT,
-                                            float* __restrict__ thr, float* __restrict__ Tq, int64_t thr_stride,
-                                            uint32_t* __restrict__ maskT, int64_t mask_stride, int ld, WaveLds& W) {
-  WaveLdsH& WH = reinterpret_cast<WaveLdsH&>(W);
-  const int half = hw_half();
-  unsigned h0 = kNoHint, h1 = kNoHint;
-#pragma unroll 1
-  for (int i = 0; i < kRunH; ++i) {
-    const int ja = j0 + i, jb0 = j0 + kRunH + i;
-    if (ja >= jend) break;
-    const bool actb = jb0 < jend;
-    const int jb = actb ? jb0 : ja;
-    LineH L;
-    L.load(K.hc + (size_t)p * kstride + (size_t)(half ? jb : ja) * kSR, (size_t)ldc * kSR, V.Mp);
-    const Pick2 hint = i == 0 ? hw_sample_hint(L, V.Mp, kappa) : Pick2{h0, h1};
-    int ok;
-    Pick2 ans;
-    cols_pair_h(V, p, ja, jb, actb, L, hint, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, WH, &ok, &ans);
-    h0 = ans.v0;
-    h1 = ans.v1;
-    HW_STAT(0, 1 + actb);
-    HW_STAT(1, !(ok & 1));
-    HW_STAT(2, actb && !(ok & 2));
-    HW_STAT(3, i == 0 ? 1 + actb : 0);
-#ifdef ACOSS_HW_NOFB  // timing ablation only (wrong results): no full-wave redo
-    continue;
-#endif
-    // the columns the fast path left: the full-wave select, from the same hints
-    if (!(ok & 1))
-      h0 = cols_body<0>(V, p, ja, ja + 1, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W,
-                        hint.v0);
-    if (actb && !(ok & 2))
-      h1 = cols_body<0>(V, p, jb, jb + 1, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W,
-                        hint.v1);
-  }
 }
 
 
@@ -2199,11 +1771,7 @@ __device__ __forceinline__ void cols_block(const ColsArgs& A, int lin, int ncb, 
   else if (KQ == 2 && V.Mp > 2048)
     cols_body<2>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
   else
-#ifdef ACOSS_HW_OFF
     cols_body<0>(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
-#else
-    cols_body_h(V, p, j0, jend, K, ldc, kstride, kappa, RT, thr, Tq, thr_stride, maskT, mask_stride, ld, W);
-#endif
 }
 
 template <int KQ>
@@ -2277,13 +1845,3 @@ int launch_crp_split(const CrpBatch& B, int nb, int L, float kappa, void* kplane
 
 }  // namespace acoss
 
-#ifdef ACOSS_HW_STATS
-extern "C" int acoss_debug_hw_stats(unsigned long long* out8) {
-  if (hipDeviceSynchronize() != hipSuccess) return ACOSS_E_HIP;
-  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(acoss::d_hw_stats), 8 * sizeof(unsigned long long)) != hipSuccess)
-    return ACOSS_E_HIP;
-  unsigned long long z[8] = {};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(acoss::d_hw_stats), z, sizeof(z)) != hipSuccess) return ACOSS_E_HIP;
-  return ACOSS_OK;
-}
-#endif

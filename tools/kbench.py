@@ -47,9 +47,3 @@ for r in range(a.reps):
     _lib.profile_enable(False)
     print("rep %d: %.1f pairs/s  %s" % (r, len(pairs) / dt, {k: round(v[0] / v[1], 3) for k, v in ph.items()}))
 print("qmax checksum", float(out["qmax"].double().sum()))
-lib = _lib.load_library()
-if hasattr(lib, "acoss_debug_hw_stats"):  # half-wave select diagnostics (ACOSS_HW_STATS builds)
-    import ctypes
-    st = (ctypes.c_ulonglong * 8)()
-    lib.acoss_debug_hw_stats(st)  # cumulative over the reps
-    print("hw stats: lines %d, fallback half0 %d, half1 %d, run starts %d" % (st[0], st[1], st[2], st[3]))
