@@ -253,6 +253,12 @@ def other_paths(nth, seed):
         ref, cdt = ef_cpu.run_pool({"mfccs": mf, "ssms": ss, "chromas": ch, "chroma_med": med}, NB, sample, nth, wd)
     gpu_rows = esc[[p * 97 % len(epairs) for p in range(ncpu)]]
     agree = int(np.sum(ref == gpu_rows))
+    # the canonical-order C oracle (oracle/ef_oracle.cpp, golden-pinned) on the same sample: the
+    # per-feature scores must be EQUAL (the GPU's CSMs follow its float order)
+    cbank = {"mfccs": mf, "ssms": ss, "chromas": ch, "chroma_med": med,
+             "off": np.arange(NT, dtype=np.int64) * NB, "nb": np.full(NT, NB, np.int32)}
+    canon = oracle.ef_batch(cbank, sample, 0.1, nthreads=nth)
+    canon_eq = int(np.sum(canon == gpu_rows[:, :3]))
     res["earlyfusion"] = {"metric": "song-pairs/s (EarlyFusion: 3 CSMs + kNN + WCSM fusion + 4 SW, 446 blocks)",
                           "value": round(len(epairs) / (ems * 1e-3), 1), "ms": round(ems, 3),
                           "pairs": int(len(epairs)), "dtype": "f32",
@@ -266,10 +272,12 @@ def other_paths(nth, seed):
                                            "sample": "%d pairs, numpy restatement + C SW oracle on %d worker "
                                                      "processes (BLAS 1 thread each), %.1f s" % (ncpu, nth, cdt)},
                           "scores_equal_to_oracle": "%d of %d" % (agree, 4 * ncpu),
-                          "scores_note": "the restatement's CSMs here are numpy/BLAS products (another float "
-                                         "summation order than the GPU's fmaf chain), so a kNN tie can flip on "
-                                         "random features; on integer-exact block features the GPU scores equal the "
-                                         "oracle composition bit for bit (tests/test_gpu_earlyfusion_pin.py)"}
+                          "feature_scores_equal_to_canonical_oracle": "%d of %d" % (canon_eq, 3 * ncpu),
+                          "scores_note": "scores_equal_to_oracle: the numpy restatement (BLAS-order CSMs, the "
+                                         "reference's own arithmetic), where a kNN tie can flip on random features; "
+                                         "feature_scores_equal_to_canonical_oracle: mfccs/ssms/chromas against "
+                                         "oracle/ef_oracle.cpp, the same float order as the GPU, pinned against the "
+                                         "reference's golden CSM/OTI/binarisation vectors (tests/test_ef_oracle.py)"}
     # ---- SNF cross-diffusion step (f2) at Da-TACOS size
     res["snf"] = snf_path(seed)
     return res
