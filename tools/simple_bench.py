@@ -56,8 +56,11 @@ def run(n, n_tracks, reps, check):
             score, _ = _lib.simple_mp_packed(flat, off, lens, pt)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        ok = bool(np.array_equal(score.cpu().numpy()[:check], np.array(ref)))
-        out["K" + kd + "r" + red] = {"pairs_per_s": round(len(pairs) * reps / dt, 1), "bitexact": ok}
+        got = score.cpu().numpy()[:check]
+        ok = bool(np.array_equal(got, np.array(ref)))
+        rel = float(np.max(np.abs(got - np.array(ref)) / np.maximum(np.abs(np.array(ref)), 1e-300)))
+        out["K" + kd + "r" + red] = {"pairs_per_s": round(len(pairs) * reps / dt, 1), "bitexact": ok,
+                                     "max_rel_diff_vs_oracle": rel}
         print(json.dumps({"n": n, "K": kd, "red": red, **out["K" + kd + "r" + red]}), flush=True)
     os.environ.pop("ACOSS_SIMPLE_K")
     return {"frames": n, "pairs": len(pairs), **out}
