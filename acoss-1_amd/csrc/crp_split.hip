@@ -371,9 +371,8 @@ __device__ __forceinline__ uint32_t gather_flags8(uint32_t acc, uint32_t s, int 
 // Unconditional histogram adds: an element outside the bins goes to this lane's own sink word
 // (the 64 words after the 128 bins, WaveLds::sink; a lane-private address, no bank conflict), so
 // every element issues the same ds_add instead of a compare, an exec-mask save / restore and a
-// masked add. Used by the window-code histogram (hist_rank_w8; ACOSS_HIST_MASKED restores the
-// masked form there, for A/B); the 16-bit-prefix histograms keep the masked add (hist_add below),
-// where the sink measured 6 % slower at 500 frames (ACOSS_HIST_SINK_PV, for A/B).
+// masked add. Used by the window-code histogram (hist_rank_w8); the 16-bit-prefix histograms keep
+// the masked add (hist_add below), where the sink measured 6 % slower at 500 frames.
 typedef __attribute__((address_space(3))) unsigned lds_u32;
 // 32-bit LDS addresses of a wave's histogram: the bins' base as an SGPR (bin address = c * 4 +
 // base in one v_lshl_add) and this lane's sink word
@@ -400,30 +399,35 @@ __device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned 
   const int lane = threadIdx.x & 63;
   reinterpret_cast<uint2*>(hist)[lane] = make_uint2(0u, 0u);
   __builtin_amdgcn_wave_barrier();
-  unsigned below = 0;
   const unsigned cmin = base8 == 0u ? 0u : 1u;  // code 0 is exact only when base8 == 0
   // every code below 127 into its bin, code 0 included (the elements at or below base8, exact
   // only when base8 == 0: a rank landing in bin 0 otherwise returns false below), so no separate
-  // count of the elements under the window; code 127 to this lane's sink. Per code: the byte (7-bit
-  // codes: the byte is the code), its bin address from an SGPR base, one select; no exec masking.
+  // count of the elements under the window; code 127 to this lane's sink; no exec masking.
+  // The sink select is done on a whole word at once (SWAR): byte k of wp = code + 1 (1..128, no
+  // carry between bytes); the bytes at 128 (code 127) get lane + 1 more, to 129 + lane; then bin
+  // index b - 1 for every byte b, so the sink of lane l is index 128 + l (A.sk). Per code one byte
+  // extract and one address, per word six ops (a per-code compare, hazard nop and select measured
+  // 0.8 % slower end to end).
   const HistAddr A(hist);
+  const unsigned lane1 = (unsigned)(lane + 1) * 0x01010101u;  // lane + 1 (<= 64) in every byte
+  const unsigned hbm = A.hb - 4u;
 #pragma unroll
   for (int h = 0; h < NW; ++h) {
+    const unsigned wp = w8[h] + 0x01010101u;
+    const unsigned H = wp & 0x80808080u;
+    const unsigned S = wp + ((H - (H >> 7)) & lane1);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const unsigned c = (w8[h] >> (8 * k)) & 0xffu;
-      const unsigned a = c < 127u ? A.hb + 4u * c : A.sk;
+      const unsigned a = hbm + 4u * ((S >> (8 * k)) & 0xffu);
       __hip_atomic_fetch_add((lds_u32*)(size_t)a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
   }
-  const int below_tot = 0;
-  (void)below;
   __builtin_amdgcn_wave_barrier();
   const uint2 hv = reinterpret_cast<const uint2*>(hist)[lane];
   const int sl = (int)(hv.x + hv.y);
   const int S = wave_incl_scan(sl);
   const int tot = __builtin_amdgcn_readlane(S, 63);
-  const int r = rho - below_tot;
+  const int r = rho;
   if (r < 0 || r >= tot) return false;
   const int E = S - sl;
   const int src = __builtin_ctzll(__ballot(E <= r && r < S));
@@ -432,7 +436,7 @@ __device__ __forceinline__ bool hist_rank_w8(const unsigned (&w8)[NW], unsigned 
   const bool second = r >= Es + h0;
   if (cmin && src == 0 && !second) return false;  // bin 0 of a window above 0: not an exact prefix
   *P = base8 + 2u * (unsigned)src + (second ? 1u : 0u);
-  *less = below_tot + Es + (second ? h0 : 0);
+  *less = Es + (second ? h0 : 0);
   *le = *less + (second ? h1 : h0);
   return true;
 }
@@ -631,8 +635,7 @@ struct Line {
   __device__ __forceinline__ unsigned min_greater_lane(unsigned x) const { return swar_min_greater(pv, x); }
   __device__ __forceinline__ unsigned min_greater(unsigned x) const { return wave_min_u32(min_greater_lane(x)); }
   static constexpr int kHalves = 1;
-  // LineS::hist_rank for the 32 elements per lane of a long line (ACOSS_NO_HIST_LONG: the search
-  // alone, for A/B)
+  // LineS::hist_rank for the 32 elements per lane of a long line
   static constexpr bool kHist = true;
   __device__ __forceinline__ bool hist_rank(unsigned hint, int rho, unsigned* hist, unsigned* P, int* le,
                                             int* less, unsigned* hbase) const {
