@@ -211,49 +211,55 @@ __global__ void k_ef_pad_rows(const float* __restrict__ X, int64_t nrows, int d,
 // of KB = 24 k-values, so each half-wave holds one whole 12-bin chroma block of a row and the
 // query rows' OTI roll (X1[12 g + c] = X[12 g + (c - oti) mod 12], wave-uniform per pair) is a
 // register rotation; needs d % 24 == 0.
-template <int KIND>
+// TILE = 64: 2 x 2 accumulators per wave; TILE = 32: one (the beat-block CSMs of short tracks,
+// M, N ~ 14..47 at Da-TACOS lengths, where a 64 x 64 tile is mostly padding).
+template <int KIND, int TILE = 64>
 __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w(const float* __restrict__ bank, int d,
                                                                 const float* __restrict__ sq, EfPairs E,
                                                                 const int* __restrict__ oti, int ld,
                                                                 int n_tiles, float* __restrict__ out) {
   constexpr int KB = KIND == 1 ? 24 : ACOSS_EF_KB, DEPTH = ACOSS_EF_DEPTH, NQ = KB / 8;  // NQ 16-byte loads per row
-  const int tiles = (ld + kT - 1) / kT;
+  constexpr int NA = TILE / 32;  // 32 x 32 accumulators per tile side
+  constexpr int NO = 2 * NA;     // operand rows per lane: NA query rows, then NA reference rows
+  const int tiles = (ld + TILE - 1) / TILE;
   const int lb = xcd_remap((int)blockIdx.x, (int)gridDim.x);
   const int tile = lb * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (tile >= n_tiles) return;
   const int p = tile / (tiles * tiles), tix = tile - p * tiles * tiles;
   int a, b, M, N;
   pair_dims(E, p, &a, &b, &M, &N);
-  const int bi = (tix / tiles) * kT, bj = (tix % tiles) * kT;
+  const int bi = (tix / tiles) * TILE, bj = (tix % tiles) * TILE;
   if (bi >= M || bj >= N) return;
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  // this lane's four operand rows (clamped into the track: rows past M / N are never stored)
-  const float* rows[4] = {bank + (E.off[a] + min(bi + r, M - 1)) * (int64_t)d + (KB / 2) * h,
-                          bank + (E.off[a] + min(bi + 32 + r, M - 1)) * (int64_t)d + (KB / 2) * h,
-                          bank + (E.off[b] + min(bj + r, N - 1)) * (int64_t)d + (KB / 2) * h,
-                          bank + (E.off[b] + min(bj + 32 + r, N - 1)) * (int64_t)d + (KB / 2) * h};
+  // this lane's operand rows (clamped into the track: rows past M / N are never stored)
+  const float* rows[NO];
+#pragma unroll
+  for (int o = 0; o < NA; ++o) {
+    rows[o] = bank + (E.off[a] + min(bi + 32 * o + r, M - 1)) * (int64_t)d + (KB / 2) * h;
+    rows[NA + o] = bank + (E.off[b] + min(bj + 32 * o + r, N - 1)) * (int64_t)d + (KB / 2) * h;
+  }
   const int nfull = d / KB;
-  f32x4e ring[DEPTH][4][NQ];
-  auto load = [&](f32x4e (&v)[4][NQ], int blk) {  // a whole block (clamped to the last whole one)
+  f32x4e ring[DEPTH][NO][NQ];
+  auto load = [&](f32x4e (&v)[NO][NQ], int blk) {  // a whole block (clamped to the last whole one)
     const int k0 = min(blk, nfull - 1) * KB;
 #pragma unroll
-    for (int o = 0; o < 4; ++o)
+    for (int o = 0; o < NO; ++o)
 #pragma unroll
       for (int q = 0; q < NQ; ++q) v[o][q] = *reinterpret_cast<const f32x4e*>(rows[o] + k0 + 4 * q);
   };
-  f32x16 acc[2][2] = {};
+  f32x16 acc[NA][NA] = {};
   const int roll = KIND == 1 ? __builtin_amdgcn_readfirstlane(oti[p]) : 0;
   // operands of steps s and s + KB / 4 come from registers 2 s and 2 s + 1 of every operand row
-  auto mul = [&](const f32x4e (&vin)[4][NQ]) {
-    f32x4e v[4][NQ];
+  auto mul = [&](const f32x4e (&vin)[NO][NQ]) {
+    f32x4e v[NO][NQ];
 #pragma unroll
-    for (int o = 0; o < 4; ++o)
+    for (int o = 0; o < NO; ++o)
 #pragma unroll
       for (int q = 0; q < NQ; ++q) v[o][q] = vin[o][q];
     if constexpr (KIND == 1) {  // rotate the query rows' 12-bin block by the pair's OTI
       if (roll) {
 #pragma unroll
-        for (int o = 0; o < 2; ++o) {
+        for (int o = 0; o < NA; ++o) {
           float e[12], t[12];
 #pragma unroll
           for (int c = 0; c < 12; ++c) e[c] = vin[o][c >> 2][c & 3];
@@ -268,9 +274,9 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w(const float* __r
         }
       }
     }
-    float op[4][KB / 2];
+    float op[NO][KB / 2];
 #pragma unroll
-    for (int o = 0; o < 4; ++o)
+    for (int o = 0; o < NO; ++o)
 #pragma unroll
       for (int s2 = 0; s2 < KB / 4; ++s2) {
         const float lo = v[o][s2 >> 1][(s2 & 1) * 2], hi = v[o][s2 >> 1][(s2 & 1) * 2 + 1];
@@ -280,12 +286,12 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w(const float* __r
         op[o][s2 + KB / 4] = __builtin_bit_cast(float, (unsigned)sw[1]);
       }
 #pragma unroll
-    for (int st = 0; st < KB / 2; ++st) {
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[0][st], op[2][st], acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[0][st], op[3][st], acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[1][st], op[2][st], acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[1][st], op[3][st], acc[1][1], 0, 0, 0);
-    }
+    for (int st = 0; st < KB / 2; ++st)
+#pragma unroll
+      for (int ti = 0; ti < NA; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < NA; ++tj)
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[ti][st], op[NA + tj][st], acc[ti][tj], 0, 0, 0);
   };
   if (nfull > 0) {
 #pragma unroll
@@ -303,7 +309,7 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w(const float* __r
   if (d % KB) {  // the partial tail block: zeros past d
     const int k0 = nfull * KB;
 #pragma unroll
-    for (int o = 0; o < 4; ++o)
+    for (int o = 0; o < NO; ++o)
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
         ring[0][o][q] = k0 + (KB / 2) * h + 4 * q < d ? *reinterpret_cast<const f32x4e*>(rows[o] + k0 + 4 * q)
@@ -312,9 +318,9 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w(const float* __r
   }
   float* ob = out + (size_t)p * ld * ld;
 #pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
+  for (int ti = 0; ti < NA; ++ti)
 #pragma unroll
-    for (int tj = 0; tj < 2; ++tj) {
+    for (int tj = 0; tj < NA; ++tj) {
       const int col = bj + 32 * tj + r;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
@@ -474,6 +480,26 @@ __device__ __forceinline__ void ef_binarize_row(const float* __restrict__ x, int
   }
 }
 
+// Rows of at most 64 columns (one key per lane) with a small nn (Da-TACOS beat blocks: N ~ 14..47,
+// nn = round(kappa N) ~ 1..5): nn rounds of (wave minimum of the remaining keys, the lowest lane
+// holding it leaves and sets its bit). Each round takes the least remaining key and, among equal
+// keys, the lowest column, so the nn lanes taken are exactly csm_to_binary's nn smallest with ties
+// to the lowest column -- the radix select's answer at a fraction of its passes.
+__device__ __forceinline__ void ef_binarize_row_knock(const float* __restrict__ x, int N, int nn, int lane,
+                                                      unsigned* bits, unsigned bit) {
+  unsigned k = lane < N ? fkey(x[lane]) : 0xffffffffu;
+  bool alive = lane < N;
+  for (int t = 0; t < nn; ++t) {  // wave-uniform
+    const unsigned m = wave_min_u32(alive ? k : 0xffffffffu);
+    const int src = __builtin_ctzll(__ballot(alive && k == m));
+    if (lane == src) {
+      alive = false;
+      atomicOr(&bits[lane], bit);
+    }
+  }
+}
+constexpr int kKnockMax = 16;  // largest nn taken by ef_binarize_row_knock
+
 __global__ __launch_bounds__(1024) void k_ef_binarize(const float* __restrict__ C, int64_t mat_stride, int ld,
                                                       EfPairs E, double kappa, uint16_t* __restrict__ Wb,
                                                       int64_t wplane, int plane0) {
@@ -489,7 +515,10 @@ __global__ __launch_bounds__(1024) void k_ef_binarize(const float* __restrict__ 
   const int row = 16 * g + w;
   if (row < M) {
     const float* xr = C + m * mat_stride + (size_t)p * ld * ld + (size_t)row * ld;
-    if (N <= 64 * 8)  // EarlyFusion's ~450-block tracks: 8 key registers halve the count passes
+    const int nn = min(kappa < 1.0 ? (int)rint(kappa * (double)N) : (int)kappa, N);  // as ef_binarize_row
+    if (N <= 64 && kappa != 0.0 && nn <= kKnockMax) {
+      if (nn > 0) ef_binarize_row_knock(xr, N, nn, lane, bits, 1u << w);
+    } else if (N <= 64 * 8)  // EarlyFusion's ~450-block tracks: 8 key registers halve the count passes
       ef_binarize_row<8>(xr, N, kappa, lane, bits, 1u << w, s_hist[w]);
     else
       ef_binarize_row<kBinRegs>(xr, N, kappa, lane, bits, 1u << w, s_hist[w]);
@@ -791,7 +820,14 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   const size_t bin_lds = (size_t)ld * 4;
   const int64_t mstride = (int64_t)mat * chunk;       // between the 3 CSM planes
   const int64_t meanstride = (int64_t)ld * chunk;     // between the 3 mean vectors
-  const int tiles = (ld + kT - 1) / kT;
+  const int tiles = (ld + kT - 1) / kT;  // LDS kernel tiles
+  // wave-tile CSMs: 32 x 32 tiles when every track has at most 64 blocks (Da-TACOS beat blocks:
+  // 14..47, a 64 x 64 tile there is mostly padding), 64 x 64 otherwise (ACOSS_EF_TILE=32|64)
+  static const int tile_env = getenv("ACOSS_EF_TILE") ? atoi(getenv("ACOSS_EF_TILE")) : 0;
+  const int wtile = (tile_env == 32 || tile_env == 64) ? tile_env : (ld <= 64 ? 32 : 64);
+  const int wtiles = (ld + wtile - 1) / wtile;
+  auto kw_euclid = wtile == 32 ? k_ef_csm_w<0, 32> : k_ef_csm_w<0, 64>;
+  auto kw_cosine = wtile == 32 ? k_ef_csm_w<1, 32> : k_ef_csm_w<1, 64>;
   int ci = 0;
   for (int64_t p0 = 0; p0 < n_pairs; p0 += chunk, ++ci) {
     const int P = (int)((n_pairs - p0) < chunk ? (n_pairs - p0) : chunk);
@@ -809,15 +845,15 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
     hipLaunchKernelGGL(k_ef_oti, dim3((P + 255) / 256), dim3(256), 0, st, chroma_med, pairs + 2 * p0, P, oti);
     ACOSS_LAUNCH_CHECK();
     {
-      const int n_tiles = tiles * tiles * P;
+      const int n_tiles = tiles * tiles * P, n_wtiles = wtiles * wtiles * P;
       auto euclid = [&](const float* bank, int d, const float* sq, float* dst) -> int {
         if (wave_tiles && d % 4 != 0 && bank == ssm && ssm_p) {
           bank = ssm_p;  // the row-padded copy made above
           d = (int)align_up((size_t)d, 4);
         }
         if (wave_tiles && d % 4 == 0)
-          hipLaunchKernelGGL(k_ef_csm_w<0>, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, st, bank, d, sq, E,
-                             oti, ld, n_tiles, dst);
+          hipLaunchKernelGGL(kw_euclid, dim3((unsigned)((n_wtiles + 3) / 4)), dim3(256), 0, st, bank, d, sq, E, oti, ld,
+                             n_wtiles, dst);
         else
           hipLaunchKernelGGL(k_ef_csm<0>, dim3((unsigned)n_tiles), dim3(256), 0, st, bank, d, sq, E, oti, ld, dst);
         ACOSS_LAUNCH_CHECK();
@@ -827,8 +863,8 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
         return ACOSS_E_HIP;
     }
     if (wave_tiles && d_chroma % 24 == 0)
-      hipLaunchKernelGGL(k_ef_csm_w<1>, dim3((unsigned)((tiles * tiles * P + 3) / 4)), dim3(256), 0, st, chn, d_chroma,
-                         nullptr, E, oti, ld, tiles * tiles * P, C + 2 * mstride);
+      hipLaunchKernelGGL(kw_cosine, dim3((unsigned)((wtiles * wtiles * P + 3) / 4)), dim3(256), 0, st, chn, d_chroma, nullptr, E,
+                         oti, ld, wtiles * wtiles * P, C + 2 * mstride);
     else
       hipLaunchKernelGGL(k_ef_csm<1>, dim3((unsigned)(tiles * tiles * P)), dim3(256), 0, st, chn, d_chroma, nullptr, E,
                          oti, ld, C + 2 * mstride);
