@@ -359,6 +359,106 @@ __global__ __launch_bounds__(64) void k_swb(const uint16_t* __restrict__ W, int6
   if (lane == 0) out[mid] = best;
 }
 
+// Small matrices (at most 64 LP rows, LP <= 32: EarlyFusion's beat-block CSMs, M ~ 14..47): a
+// group of LP lanes per matrix (lane ll of a group owns rows 8 ll .. 8 ll + 7, one band), G = 64 /
+// LP matrices per wave instead of one matrix per wave with most lanes idle. The same cell
+// recurrence in the same order as k_swb<8>, so the same scores bit for bit.
+__global__ __launch_bounds__(64) void k_swb_grp(const uint16_t* __restrict__ W, int64_t wstride, int ldw,
+                                                const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                                                int n, int LP, double* __restrict__ out) {
+  constexpr int R = 8;
+  constexpr unsigned kMask = (1u << R) - 1;
+  __shared__ double s_best[64];
+  const int lane = threadIdx.x;
+  const int G = 64 / LP;
+  const int g = lane / LP, ll = lane - g * LP;
+  const int mid = blockIdx.x * G + g;
+  const bool in_group = g < G && mid < n;
+  const int M = in_group ? rows[mid] : 0, N = in_group ? cols[mid] : 0;
+  const bool live = in_group && M >= 4 && N >= 4;
+  const int row0 = ll * R;
+  const bool rows_ok = live && row0 < M;
+  const uint16_t* wr = W + (size_t)(in_group ? mid : 0) * wstride + (size_t)(row0 >> 4) * ldw;
+  const int sh = row0 & 15;
+  auto word = [&](int c) -> unsigned {
+    return (rows_ok && c >= 0 && c < N) ? (((unsigned)wr[c] >> sh) & kMask) : 0u;
+  };
+  double s1[R], s2[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) s1[r] = s2[r] = 0.0;
+  unsigned w1 = 0, w2 = 0, w3 = 0;
+  SwAbove h1{0, 0, 0}, h2{0, 0, 0}, h3{0, 0, 0};
+  double pa = 0.0, pb = 0.0, best = 0.0;
+  unsigned pbits = 0;
+  unsigned q0 = word(-ll), q1 = word(1 - ll), q2 = word(2 - ll), q3 = word(3 - ll);
+  // steps until every group of the wave is done (wave-uniform bound)
+  const int S_end = (int)wave_max_u32(live ? (unsigned)(N + LP - 1) : 0u);
+  for (int s = 0; s < S_end; ++s) {
+    const int c = s - ll;
+    const unsigned w0 = q0;
+    q0 = q1;
+    q1 = q2;
+    q2 = q3;
+    q3 = word(c + 4);
+    SwAbove h0;
+    h0.sa = __shfl_up(pa, 1);
+    h0.sb = __shfl_up(pb, 1);
+    h0.b = (unsigned)__shfl_up((int)pbits, 1);
+    if (ll == 0) {  // the group's first rows: nothing above
+      h0.sa = h0.sb = 0.0;
+      h0.b = 0;
+    }
+    const uint32_t e1 = (w1 << 3) | h1.b;
+    const uint32_t e2 = (w2 << 3) | h2.b;
+    const uint32_t e3 = (w3 << 3) | h3.b;
+    const bool cok = c >= 3 && c < N;
+    double s0[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double A = r >= 1 ? s1[r - 1] : h1.sb;
+      const double Bv = r >= 2 ? s1[r - 2] : (r == 1 ? h1.sb : h1.sa);
+      const double Cv = r >= 1 ? s2[r - 1] : h2.sb;
+      const double mv = ((e1 >> (r + 2)) & 1) ? 1.0 : -1.0;
+      const double d1 = ((e2 >> (r + 1)) & 1) ? 0.0 : -0.7;
+      const double d2 = ((e2 >> r) & 1) ? 0.0 : -0.7;
+      const double d3 = ((e3 >> (r + 1)) & 1) ? 0.0 : -0.7;
+      const double x1 = (A + mv) + d1;
+      const double x2 = (Bv + mv) + d2;
+      const double x3 = (Cv + mv) + d3;
+      double v = x1;
+      v = x2 > v ? x2 : v;
+      v = x3 > v ? x3 : v;
+      v = 0.0 > v ? 0.0 : v;
+      const int i = row0 + r;
+      v = (cok && i >= 3 && i < M) ? v : 0.0;
+      best = v > best ? v : best;
+      s0[r] = v;
+    }
+    pa = s0[R - 2];
+    pb = s0[R - 1];
+    pbits = (w0 >> (R - 3)) & 7u;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      s2[r] = s1[r];
+      s1[r] = s0[r];
+    }
+    w3 = w2;
+    w2 = w1;
+    w1 = w0;
+    h3 = h2;
+    h2 = h1;
+    h1 = h0;
+  }
+  // per-group maximum through LDS (groups need not be a power of two wide)
+  s_best[lane] = best;
+  __syncthreads();
+  if (in_group && ll == 0) {
+    double m = 0.0;
+    for (int k = 0; k < LP; ++k) m = s_best[lane + k] > m ? s_best[lane + k] : m;
+    out[mid] = live ? m : 0.0;
+  }
+}
+
 // Byte matrices (acoss_sw_constrained's layout) -> bit planes; flags elements other than 0/1.
 __global__ void k_sw_pack(const uint8_t* __restrict__ mats, const int64_t* __restrict__ off,
                           const int32_t* __restrict__ rows, const int32_t* __restrict__ cols, uint16_t* __restrict__ W,
@@ -397,7 +497,12 @@ size_t sw_bnd_bytes(int max_rows, int max_cols) {
 int launch_swb_batch(const uint16_t* W, int64_t wstride, int ldw, const int32_t* rows, const int32_t* cols, int n,
                      int max_rows, int max_cols, void* bnd, double* out, hipStream_t s) {
   const int64_t bstride = (int64_t)(sw_bnd_bytes(max_rows, max_cols) / 32);
-  if (sw_rows_per_lane(max_rows) == 8)
+  const int LP = (max_rows + 7) / 8;  // lanes per matrix at 8 rows per lane
+  if (LP <= 32) {  // two or more matrices per wave (Da-TACOS EarlyFusion: +18 % over one per wave)
+    const int G = 64 / LP;
+    hipLaunchKernelGGL(k_swb_grp, dim3((unsigned)((n + G - 1) / G)), dim3(64), 0, s, W, wstride, ldw, rows, cols, n, LP,
+                       out);
+  } else if (sw_rows_per_lane(max_rows) == 8)
     hipLaunchKernelGGL(k_swb<8>, dim3(n), dim3(64), 0, s, W, wstride, ldw, rows, cols, static_cast<double4*>(bnd),
                        bstride, out);
   else
