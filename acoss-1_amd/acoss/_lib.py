@@ -540,11 +540,25 @@ def earlyfusion(bank, pairs, kappa=0.1, K=10, mu=0.5):
     if P == 0:
         return out
     _check_ef_neighbours(bank, pairs, kappa, K)
+    T = int(bank["nb"].shape[0])
+    order = None
+    if P > 4096:
+        # pairs in (reference band, query) order: a band of 32 reference tracks' block rows stays
+        # cache-resident while every query track's rows stream past it once per band (an i-major
+        # pair list streams every reference track's rows once per query). Scores go back to the
+        # caller's order. Da-TACOS shape, 15,000 songs: 3.29M -> 4.07M pairs/s (bands of 16..128
+        # alike; profiles/r05/ef_short/efband15k_*.log).
+        key = (pairs[:, 1].to(torch.int64) // 32) * T + pairs[:, 0].to(torch.int64)
+        order = torch.argsort(key, stable=True)
+        pairs = pairs[order].contiguous()
+    dst = out if order is None else torch.empty_like(out)
     rc = lib.acoss_earlyfusion(_ptr(bank["mfccs"]), _ptr(bank["ssms"]), _ptr(bank["chromas"]), _ptr(bank["chroma_med"]),
-                               _ptr(bank["off"]), _ptr(bank["nb"]), int(bank["nb"].shape[0]), int(bank["max_blocks"]),
+                               _ptr(bank["off"]), _ptr(bank["nb"]), T, int(bank["max_blocks"]),
                                int(bank["mfccs"].shape[1]), int(bank["ssms"].shape[1]), int(bank["chromas"].shape[1]),
-                               _ptr(pairs), int(P), float(kappa), int(K), float(mu), _ptr(out), _stream())
+                               _ptr(pairs), int(P), float(kappa), int(K), float(mu), _ptr(dst), _stream())
     _check(rc, "acoss_earlyfusion")
+    if order is not None:
+        out[order] = dst
     return out
 
 
