@@ -528,6 +528,40 @@ __global__ __launch_bounds__(1024) void k_ef_binarize(const float* __restrict__ 
   for (int c = threadIdx.x; c < N; c += 1024) o[c] = (uint16_t)bits[c];
 }
 
+// k_ef_binarize for batches whose tracks all have at most 64 blocks (Da-TACOS beat blocks): ONE
+// 256-thread block per (pair, matrix) instead of a 1024-thread block per 16 rows; wave w takes
+// rows w, w + 4, ... with the same per-row selects as k_ef_binarize, into LDS words of 16 rows.
+__global__ __launch_bounds__(256) void k_ef_binarize_small(const float* __restrict__ C, int64_t mat_stride, int ld,
+                                                           EfPairs E, double kappa, uint16_t* __restrict__ Wb,
+                                                           int64_t wplane, int plane0) {
+  __shared__ unsigned bits[4][64];
+  __shared__ __attribute__((aligned(16))) unsigned s_hist[4][256 + 64];  // radix_kth, one per wave
+  const int p = blockIdx.x, m = blockIdx.y;
+  int a, b, M, N;
+  pair_dims(E, p, &a, &b, &M, &N);
+  for (int e = threadIdx.x; e < 4 * 64; e += 256) bits[e >> 6][e & 63] = 0u;
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nn = min(kappa < 1.0 ? (int)rint(kappa * (double)N) : (int)kappa, N);  // as ef_binarize_row
+  for (int row = w; row < M; row += 4) {
+    const float* xr = C + m * mat_stride + (size_t)p * ld * ld + (size_t)row * ld;
+    unsigned* brow = bits[row >> 4];
+    const unsigned bit = 1u << (row & 15);
+    if (kappa != 0.0 && nn <= kKnockMax) {
+      if (nn > 0) ef_binarize_row_knock(xr, N, nn, lane, brow, bit);
+    } else {
+      ef_binarize_row<8>(xr, N, kappa, lane, brow, bit, s_hist[w]);
+    }
+  }
+  __syncthreads();
+  const int ng = (M + 15) / 16;
+  uint16_t* o = Wb + ((size_t)p * 4 + plane0 + m) * wplane;
+  for (int e = threadIdx.x; e < ng * 64; e += 256) {
+    const int g = e >> 6, c = e & 63;
+    if (c < N) o[(size_t)g * ld + c] = (uint16_t)bits[g][c];
+  }
+}
+
 // Mean of the k smallest of each row (COLS = false) or column; blockIdx.z = matrix.
 template <bool COLS>
 __global__ __launch_bounds__(256) void k_ef_kmean(const float* __restrict__ C, int64_t mat_stride, int ld, EfPairs E,
@@ -827,6 +861,9 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   const int wtile = (tile_env == 32 || tile_env == 64) ? tile_env : (ld <= 64 ? 32 : 64);
   const int wtiles = (ld + wtile - 1) / wtile;
   auto kw_euclid = wtile == 32 ? k_ef_csm_w<0, 32> : k_ef_csm_w<0, 64>;
+  // one binarize block per (pair, matrix) when every track has at most 64 blocks (15,000 Da-TACOS-
+  // shape songs: 4.04M -> 4.38M pairs/s, profiles/r05/ef_short/efbin15k_*.log)
+  const bool small_bin = ld <= 64;
   auto kw_cosine = wtile == 32 ? k_ef_csm_w<1, 32> : k_ef_csm_w<1, 64>;
   int ci = 0;
   for (int64_t p0 = 0; p0 < n_pairs; p0 += chunk, ++ci) {
@@ -871,8 +908,11 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_CSM, st);
     prof_begin(PH_BIN, st);
-    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 3), dim3(1024), bin_lds, st, C, mstride, ld, E, kappa,
-                       Wb, wplane, 0);
+    if (small_bin)
+      hipLaunchKernelGGL(k_ef_binarize_small, dim3(P, 3), dim3(256), 0, st, C, mstride, ld, E, kappa, Wb, wplane, 0);
+    else
+      hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 3), dim3(1024), bin_lds, st, C, mstride, ld, E, kappa,
+                         Wb, wplane, 0);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_BIN, st);
     prof_begin(PH_WCSM, st);
@@ -903,8 +943,11 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_WCSM, st);
     prof_begin(PH_BIN, st);
-    hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 1), dim3(1024), bin_lds, st, C, mstride, ld, E, kappa,
-                       Wb, wplane, 3);
+    if (small_bin)
+      hipLaunchKernelGGL(k_ef_binarize_small, dim3(P, 1), dim3(256), 0, st, C, mstride, ld, E, kappa, Wb, wplane, 3);
+    else
+      hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 1), dim3(1024), bin_lds, st, C, mstride, ld, E, kappa,
+                         Wb, wplane, 3);
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_BIN, st);
     prof_begin(PH_SW, st);
