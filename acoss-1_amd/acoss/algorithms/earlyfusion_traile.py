@@ -70,6 +70,7 @@ class EarlyFusion(CoverAlgorithm):
         if log_times:
             self.times = {'features': [], 'raw': []}
         self._dev = {}
+        self._pending = []  # background cache writes (flush_cache)
         CoverAlgorithm.__init__(self, dataset_csv=dataset_csv, name="EarlyFusionTraile", datapath=datapath,
                                 shortname=shortname, similarity_types=["mfccs", "ssms", "chromas", "early"],
                                 cachedir=cachedir)
@@ -116,12 +117,36 @@ class EarlyFusion(CoverAlgorithm):
             bf = {"mfccs": host["mfccs"][b0:b0 + nb], "ssms": host["ssms"][b0:b0 + nb],
                   "chromas": host["chromas"][b0:b0 + nb], "chroma_med": host["chroma_med"][t]}
             self.all_block_feats[i] = bf
-            if write_cache:
-                _save_feature_file("%s_%i.h5" % (self.get_cacheprefix(), i), bf)
+            if write_cache:  # on a background thread: ~1 ms of np.savez per song (15 s at 15,000 songs)
+                self._pending.append(self._cache_writer().submit(
+                    _save_feature_file, "%s_%i.h5" % (self.get_cacheprefix(), i), bf))
             res.append(bf)
         if self.log_times:
             self.times['features'].append((time.time() - tic) / max(1, len(idx)))
         return res
+
+    def _cache_writer(self):
+        """One background thread for the block-feature disk cache, so the ~1 ms np.savez per song
+        overlaps the GPU work that follows prepare() instead of adding to it."""
+        if getattr(self, "_writer", None) is None:
+            import atexit
+            from concurrent.futures import ThreadPoolExecutor
+            self._writer = ThreadPoolExecutor(max_workers=1)
+            atexit.register(self.flush_cache)
+        return self._writer
+
+    def flush_cache(self):
+        """Wait until every block-feature cache file of prepare() is on disk (re-raises a failed
+        write); all_pairwise and interpreter exit call it."""
+        pending, self._pending = self._pending, []
+        for f in pending:
+            f.result()
+
+    def all_pairwise(self, *args, **kwargs):
+        try:
+            return CoverAlgorithm.all_pairwise(self, *args, **kwargs)
+        finally:
+            self.flush_cache()
 
     def _device(self, i):
         if i not in self._dev:
