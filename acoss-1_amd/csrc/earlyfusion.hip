@@ -856,9 +856,8 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   const int64_t meanstride = (int64_t)ld * chunk;     // between the 3 mean vectors
   const int tiles = (ld + kT - 1) / kT;  // LDS kernel tiles
   // wave-tile CSMs: 32 x 32 tiles when every track has at most 64 blocks (Da-TACOS beat blocks:
-  // 14..47, a 64 x 64 tile there is mostly padding), 64 x 64 otherwise (ACOSS_EF_TILE=32|64)
-  static const int tile_env = getenv("ACOSS_EF_TILE") ? atoi(getenv("ACOSS_EF_TILE")) : 0;
-  const int wtile = (tile_env == 32 || tile_env == 64) ? tile_env : (ld <= 64 ? 32 : 64);
+  // 14..47, a 64 x 64 tile there is mostly padding; profiles/r05/ef_short), 64 x 64 otherwise
+  const int wtile = ld <= 64 ? 32 : 64;
   const int wtiles = (ld + wtile - 1) / wtile;
   auto kw_euclid = wtile == 32 ? k_ef_csm_w<0, 32> : k_ef_csm_w<0, 64>;
   // one binarize block per (pair, matrix) when every track has at most 64 blocks (15,000 Da-TACOS-

@@ -89,9 +89,16 @@ def test_crp_pair_degenerate_rows(M, N, silence):
     np.testing.assert_array_equal(got["crp"].cpu().numpy(), ref["crp"])
 
 
-@pytest.mark.parametrize("path", ["split", "fused"])
+@pytest.mark.parametrize("path", [
+    "split", "fused",
+    # the alternative kernels the runtime switches select (read once per process, hence the
+    # subprocess): generic LDS-Gram select and mask on the fused path, the one-pair-per-wave and
+    # the general DP, the f32 chen17 DP instead of the packed one, no lane-strided short lines
+    "fused:ACOSS_SELECT_GENERIC=1:ACOSS_MASK_GENERIC=1",
+    "split:ACOSS_DP_NOGROUP=1", "split:ACOSS_DP_NOFAST=1", "split:ACOSS_DP_F32=1", "split:ACOSS_NO_SHORT=1"])
 def test_crp_align_degenerate_batch(path, monkeypatch):
-    """Batch path on silences / ragged lengths / long tracks, both CRP implementations."""
+    """Batch path on silences / ragged lengths / long tracks, both CRP implementations and every
+    alternative kernel behind a runtime switch: each equal to the oracle."""
     import subprocess
     import sys
     import os
@@ -118,7 +125,9 @@ assert np.array_equal(got["dmax"].cpu().numpy(), d)
 print("ok")
 ''' % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
        os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "acoss-1_amd"))
-    env = dict(os.environ, ACOSS_CRP_PATH=path)
+    parts = path.split(":")
+    env = dict(os.environ, ACOSS_CRP_PATH=parts[0])
+    env.update(kv.split("=", 1) for kv in parts[1:])
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 

@@ -271,3 +271,65 @@ def test_earlyfusion_scores_equal_canonical_oracle_on_float_blocks():
         for f, key in enumerate(("mfccs", "ssms", "chromas")):
             bad = np.flatnonzero(got[:, f] != ref[:, f])
             assert len(bad) == 0, (kappa, key, len(bad), pairs[bad[:5]], got[bad[:5], f], ref[bad[:5], f])
+
+
+_EF_SHORT_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [sys.argv[1], sys.argv[1] + '/acoss-1_amd']
+from acoss import _lib
+rng = np.random.default_rng(21)
+NT = 96
+nb = rng.integers(14, 48, size=NT).astype(np.int32)  # Da-TACOS beat-block counts
+off = np.concatenate([[0], np.cumsum(nb[:-1])]).astype(np.int64)
+R = int(nb.sum())
+bank = {'mfccs': torch.as_tensor(rng.standard_normal((R, 1000), dtype=np.float32)).cuda(),
+        'ssms': torch.as_tensor(np.abs(rng.standard_normal((R, 1225), dtype=np.float32))).cuda(),
+        'chromas': torch.as_tensor(np.abs(rng.standard_normal((R, 480), dtype=np.float32))).cuda(),
+        'chroma_med': torch.as_tensor(np.abs(rng.standard_normal((NT, 12), dtype=np.float32))).cuda(),
+        'off': torch.as_tensor(off).cuda(), 'nb': torch.as_tensor(nb).cuda(), 'max_blocks': int(nb.max())}
+pairs = np.array([(i, j) for i in range(NT) for j in range(NT) if i != j], np.int32)
+if sys.argv[3] == 'slices':  # calls of <= 4096 pairs: processed in the caller's order
+    out = np.concatenate([_lib.earlyfusion(bank, pairs[k:k + 4000], 0.1, 10).cpu().numpy()
+                          for k in range(0, len(pairs), 4000)])
+else:  # one call of 9120 pairs: (reference band, query) order inside, scattered back
+    out = _lib.earlyfusion(bank, pairs, 0.1, 10).cpu().numpy()
+np.save(sys.argv[2], out)
+"""
+
+
+def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
+    """Da-TACOS-sized tracks (14..47 beat blocks: 32 x 32 CSM tiles, the knockout binarize, one
+    binarize block per matrix, several Smith-Waterman matrices per wave): the scores of one
+    9,120-pair call (processed in (reference band, query) order and scattered back) equal those of
+    4,000-pair calls in the caller's order, and those of many small chunks on one stream
+    (ACOSS_EF_BYTES / ACOSS_EF_STREAMS, read once per process, hence separate processes), bit for
+    bit."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    out = {}
+    for tag, mode, env in (("band", "one", {}), ("slices", "slices", {}),
+                           ("chunks", "one", {"ACOSS_EF_STREAMS": "1", "ACOSS_EF_BYTES": str(8 << 20)})):
+        f = str(tmp_path / ("%s.npy" % tag))
+        r = subprocess.run([sys.executable, "-c", _EF_SHORT_SCRIPT, ROOT, f, mode],
+                           env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[tag] = np.load(f)
+    assert np.isfinite(out["band"]).all() and out["band"].shape == (96 * 95, 4)
+    np.testing.assert_array_equal(out["band"], out["slices"])
+    np.testing.assert_array_equal(out["band"], out["chunks"])
+    # and the feature scores of a sample of pairs == the canonical-order oracle (same bank)
+    import oracle
+    rng = np.random.default_rng(21)
+    nb = rng.integers(14, 48, size=96).astype(np.int32)
+    R = int(nb.sum())
+    bank = {"mfccs": rng.standard_normal((R, 1000), dtype=np.float32),
+            "ssms": np.abs(rng.standard_normal((R, 1225), dtype=np.float32)),
+            "chromas": np.abs(rng.standard_normal((R, 480), dtype=np.float32)),
+            "chroma_med": np.abs(rng.standard_normal((96, 12), dtype=np.float32)),
+            "nb": nb, "off": np.concatenate([[0], np.cumsum(nb[:-1])]).astype(np.int64)}
+    pairs = np.array([(i, j) for i in range(96) for j in range(96) if i != j], np.int32)
+    idx = np.random.default_rng(3).choice(len(pairs), 150, replace=False)
+    ref = oracle.ef_batch(bank, pairs[idx], 0.1)
+    np.testing.assert_array_equal(out["band"][idx, :3], np.asarray(ref, np.float64)[:, :3])
