@@ -75,6 +75,7 @@ def test_full_corpus_qmax_and_map_parity_500():
     {"ACOSS_SPLIT_STREAMS": "3", "ACOSS_KEY_BYTES": str(40 << 20)},
     {"ACOSS_BATCH_PAIRS": "5", "ACOSS_SPLIT_STREAMS": "1", "ACOSS_KEY_BYTES": "1"},  # 1 pair per sub-batch
     {"ACOSS_SPLIT_STREAMS": "2", "ACOSS_KEY_BYTES": "1"},         # 1-pair sub-batches on two streams
+    {"ACOSS_WS_BYTES": str(48 << 20)},                            # DP batches from a small workspace budget
 ])
 def test_batching_branches_ragged(monkeypatch, env):
     from acoss.engine import ChromaBank
