@@ -154,6 +154,13 @@ def test_earlyfusion_composition(tmp_path, monkeypatch):
     csv, fdir, tracks, labels = _dataset(tmp_path, frames=3000, mfcc=True, n_cliques=12)
     ef = EarlyFusion(csv, fdir, shortname="t", cachedir=str(tmp_path / "cache"))
     ef.all_pairwise(symmetric=True)
+    # the block-feature disk cache (written on a background thread, flushed by all_pairwise):
+    # every song's file is there and reads back to the arrays in memory
+    from acoss.features_io import load_features
+    for i in range(ef.N):
+        cached = load_features("%s_%i.h5" % (ef.get_cacheprefix(), i))
+        for k in ("mfccs", "ssms", "chromas", "chroma_med"):
+            np.testing.assert_array_equal(np.asarray(cached[k]), np.asarray(ef.all_block_feats[i][k]))
     for (i, j) in [(0, 1), (1, 4), (2, 3)]:
         f1, f2 = ef.load_features(i), ef.load_features(j)
         mats = [m.cpu().numpy() for m in ef.pair_matrices(i, j)]
