@@ -613,12 +613,16 @@ __global__ __launch_bounds__(256) void k_ef_kmean(const float* __restrict__ C, i
 // reference's np.mean over np.partition output has unspecified order: tolerance).
 template <bool COLS, int KMAX, int KC = 0>  // KC > 0: k fixed at compile time (k = KC = KMAX)
 __global__ __launch_bounds__(256) void k_ef_kmin(const float* __restrict__ C, int64_t mat_stride, int ld, EfPairs E,
-                                                 int k_rt, float* __restrict__ out, int64_t omat_stride) {
+                                                 int k_rt, float* __restrict__ out, int64_t omat_stride, int ppb,
+                                                 int n_pairs) {
   const int k = KC ? KC : k_rt;
-  const int p = blockIdx.y, m = blockIdx.z;
+  // ppb pairs per block (short tracks: 4 pairs x 64 lines per 256-thread block, ld <= 64)
+  const int lpb = 256 / ppb;
+  const int p = blockIdx.y * ppb + (int)threadIdx.x / lpb, m = blockIdx.z;
+  if (p >= n_pairs) return;
   int a, b, M, N;
   pair_dims(E, p, &a, &b, &M, &N);
-  const int line = blockIdx.x * blockDim.x + threadIdx.x;
+  const int line = blockIdx.x * lpb + (int)threadIdx.x % lpb;
   const int nl = COLS ? N : M, len = COLS ? M : N;
   if (line >= nl) return;
   const float* base = C + m * mat_stride + (size_t)p * ld * ld + (COLS ? (size_t)line : (size_t)line * ld);
@@ -863,6 +867,9 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   // one binarize block per (pair, matrix) when every track has at most 64 blocks (15,000 Da-TACOS-
   // shape songs: 4.04M -> 4.38M pairs/s, profiles/r05/ef_short/efbin15k_*.log)
   const bool small_bin = ld <= 64;
+  // column k-smallest means: 4 pairs per 256-thread block when every track has at most 64 blocks
+  const int kmin_ppb = ld <= 64 ? 4 : 1;
+  const unsigned kmin_gx = ld <= 64 ? 1u : (unsigned)((ld + 255) / 256);
   auto kw_cosine = wtile == 32 ? k_ef_csm_w<1, 32> : k_ef_csm_w<1, 64>;
   int ci = 0;
   for (int64_t p0 = 0; p0 < n_pairs; p0 += chunk, ++ci) {
@@ -919,15 +926,15 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
       hipLaunchKernelGGL((k_ef_kmin_rows<10, 10>), dim3((ld + 63) / 64, P, 3), dim3(64), 0, st, C, mstride, ld, E,
                          (int)K, rmean, meanstride);
       ACOSS_LAUNCH_CHECK();
-      hipLaunchKernelGGL((k_ef_kmin<true, 10, 10>), dim3((ld + 255) / 256, P, 3), dim3(256), 0, st, C, mstride, ld,
-                         E, (int)K, cmean, meanstride);
+      hipLaunchKernelGGL((k_ef_kmin<true, 10, 10>), dim3(kmin_gx, (P + kmin_ppb - 1) / kmin_ppb, 3), dim3(256), 0, st,
+                         C, mstride, ld, E, (int)K, cmean, meanstride, kmin_ppb, P);
       ACOSS_LAUNCH_CHECK();
     } else if (K <= kKmax) {
       hipLaunchKernelGGL((k_ef_kmin_rows<kKmax>), dim3((ld + 63) / 64, P, 3), dim3(64), 0, st, C, mstride, ld, E,
                          (int)K, rmean, meanstride);
       ACOSS_LAUNCH_CHECK();
-      hipLaunchKernelGGL((k_ef_kmin<true, kKmax>), dim3((ld + 255) / 256, P, 3), dim3(256), 0, st, C, mstride, ld, E,
-                         (int)K, cmean, meanstride);
+      hipLaunchKernelGGL((k_ef_kmin<true, kKmax>), dim3(kmin_gx, (P + kmin_ppb - 1) / kmin_ppb, 3), dim3(256), 0, st,
+                         C, mstride, ld, E, (int)K, cmean, meanstride, kmin_ppb, P);
       ACOSS_LAUNCH_CHECK();
     } else {
       hipLaunchKernelGGL(k_ef_kmean<false>, dim3((ld + 3) / 4, P, 3), dim3(256), 0, st, C, mstride, ld, E, (int)K,
