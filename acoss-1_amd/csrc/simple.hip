@@ -546,8 +546,11 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
   const int ngmax = (2 * max(max_len - kFastL + 1, 1) - 1 + 64 * kdiag - 1) / (64 * kdiag);
   // a pair with at most 2 groups goes to ONE wave (it walks both: no wave of the block idles
   // while its partner finishes the longer group; 200 frames: 6.02M vs 4.95M pairs/s with 2 waves)
+  // pairs of up to 8 groups (tracks up to ~1,030 frames, Da-TACOS lengths) two per block, two
+  // waves each (500 frames: +6-9 %; 2,000 frames: -14 %, one pair per block stays there;
+  // profiles/r05/simple_k/)
   const char* penv = getenv("ACOSS_SIMPLE_PPB");
-  int ppb = penv ? atoi(penv) : (ngmax <= 2 ? 4 : 1);
+  int ppb = penv ? atoi(penv) : (ngmax <= 2 ? 4 : (ngmax <= 8 ? 2 : 1));
   if (ppb != 1 && ppb != 2 && ppb != 4) ppb = 1;
   while (ppb > 1 && (size_t)ppb * (n2max + align_up((size_t)max_len, 2)) * 8 > 96 * 1024) ppb /= 2;
   // row minima through LDS chunks for packed short pairs, per-step DPP minima for long ones
