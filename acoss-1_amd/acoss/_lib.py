@@ -44,6 +44,7 @@ SIGNATURES = {
     "acoss_get_oti": [_vp, _vp, _i32, _vp, _vp],
     "acoss_binarize_rows": [_vp, _i32, _i32, _i32, _vp, _vp],
     "acoss_wcsm": [_vp, _i32, _i32, _i32, _i32, _f32, _vp, _vp],
+    "acoss_neg_exp": [_vp, _i64, _vp, _vp],
     "acoss_snf_step": [_vp, _i32, _i32, _i32, _vp, _vp, _i32, ctypes.c_double, _vp, _i32, _vp],
     "acoss_snf_diffuse_rows": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i32, _vp],
     "acoss_snf_left_rows": [_vp, _i32, _i32, _i32, _vp, _vp, _i32, ctypes.c_double, _vp, _i32, _vp],
@@ -324,6 +325,18 @@ def wcsm(CSM, k1, k2, mu=0.5):
     out = torch.empty(C.shape, dtype=torch.float32, device="cuda")
     rc = lib.acoss_wcsm(_ptr(C), int(C.shape[0]), int(C.shape[1]), int(k1), int(k2), float(mu), _ptr(out), _stream())
     _check(rc, "acoss_wcsm")
+    return out
+
+
+def neg_exp(x):
+    """exp(-x) elementwise in the canonical float32 exp (acoss_neg_exp; the early matrix of
+    EarlyFusion, earlyfusion_traile.py:182)."""
+    torch = _torch()
+    lib = load_library()
+    X = _dev(x, torch.float32)
+    out = torch.empty(X.shape, dtype=torch.float32, device="cuda")
+    rc = lib.acoss_neg_exp(_ptr(X), int(X.numel()), _ptr(out), _stream())
+    _check(rc, "acoss_neg_exp")
     return out
 
 

@@ -65,6 +65,31 @@ def _on_gpu():
         return False
 
 
+class _RootOnlyDs(dict):
+    """Ds on a rank > 0 after a gather onto rank 0 (Serra09, SiMPle under torch.distributed): the
+    similarity types are still listed, but reading a matrix raises instead of silently returning
+    the zeros of a matrix this rank never received. The memmaps are dropped, which
+    frees their unlinked files' disk blocks."""
+
+    def __init__(self, Ds, rank):
+        dict.__init__(self, {k: None for k in Ds})
+        self._rank = rank
+
+    def __getitem__(self, key):
+        if key not in self:
+            raise KeyError(key)
+        raise RuntimeError(
+            "Ds[%r] was gathered onto rank 0 only; rank %d does not hold it. Read Ds on rank 0, or set "
+            "algorithm.Ds_on_every_rank = True before all_pairwise to all-gather it onto every rank "
+            "(INTEGRATION.md section 3)." % (key, self._rank))
+
+    def values(self):
+        return [self[k] for k in self]  # raises on the first key
+
+    def items(self):
+        return [(k, self[k]) for k in self]
+
+
 class CoverAlgorithm(object):
     def __init__(self, dataset_csv, name="Serra09", datapath="features_benchmark", shortname="full",
                  cachedir="cache", similarity_types=["main"]):
@@ -88,6 +113,8 @@ class CoverAlgorithm(object):
     # Ds assembled on every rank (all-gather) instead of rank 0 only (gather): subclasses whose
     # late fusion runs on every rank after all_pairwise (ChenFusion, EarlyFusion) set this
     _Ds_on_every_rank = False
+    # the same, opted into by a caller that reads Ds on every rank (an instance attribute)
+    Ds_on_every_rank = False
 
     def _new_dmat(self, s, rank):
         """Ds[s] as a float32 (N, N) memmap (:61). Rank r > 0's file is unlinked once mapped: the
@@ -175,21 +202,21 @@ class CoverAlgorithm(object):
 
     def all_pairwise(self, parallel=0, n_cores=12, symmetric=False, precomputed=False):
         prefix = self.get_cacheprefix()
+        world, rank = _dist_info()
+        if world > 1:  # before ANY "cuda" allocation, the precomputed path's evaluation included
+            _dist.bind_local_device()
         if precomputed:
             self._load_Ds(prefix)
             self.get_all_clique_ids()
             self._holds_Ds, self._stats_from_root = True, False
             return
-        world, rank = _dist_info()
-        if world > 1:
-            _dist.bind_local_device()
         self.prepare()
         if world > 1:
             bounds = _dist.stripe_bounds(self.track_lengths(), world, symmetric, m=0, tau=0)
         else:
             bounds = [(0, self.N)]
         r0, r1 = bounds[rank]
-        every = world == 1 or self._Ds_on_every_rank
+        every = world == 1 or self._Ds_on_every_rank or self.Ds_on_every_rank
         self._holds_Ds = every or rank == 0
         self._stats_from_root = not every
         if not self._device_all_pairwise(bounds, r0, r1, world, symmetric, every):
@@ -200,6 +227,8 @@ class CoverAlgorithm(object):
             if symmetric and self._holds_Ds:
                 for key in self.Ds:
                     self.Ds[key] += self.Ds[key].T
+        if not self._holds_Ds:  # reading Ds here is a caller error: make it a loud one
+            self.Ds = _RootOnlyDs(self.Ds, rank)
         if rank == 0:
             self._save_Ds(prefix)
 
@@ -263,9 +292,12 @@ class CoverAlgorithm(object):
 
     def _finish_device(self, norm, mode):
         """normalize_by_length on the device for every Ds key (acoss_ds_finish, mode 'serra09' or
-        'chen'): one upload, one HIP kernel, one download per matrix."""
-        import torch
+        'chen'): one upload, one HIP kernel, one download per matrix. A rank that does not hold
+        the gathered matrices has nothing to normalise."""
+        if not self._holds_Ds:
+            return
         from .. import _lib
+        torch = _lib._torch()  # binds this rank's GPU (nccl) before the first "cuda" allocation
         norm = np.asarray(norm, np.float64)
         for key in list(self.Ds):
             D = torch.as_tensor(np.ascontiguousarray(self.Ds[key], np.float32)).cuda()
@@ -315,7 +347,10 @@ class CoverAlgorithm(object):
         a row to 'results_<shortname>_<name>.csv'. Under torch.distributed only rank 0 prints and
         writes the row (one row per call, as the reference's single process writes). When Ds was
         gathered onto rank 0 only, rank 0 computes the statistics and broadcasts them, so every rank
-        must call this (coverid.benchmark does) and every rank returns the same values."""
+        must call this (coverid.benchmark does) and every rank returns the same values: a
+        collective call, like the gather before it. Set
+        `Ds_on_every_rank = True` before all_pairwise to all-gather Ds onto every rank instead;
+        each rank then evaluates on its own, without any collective here."""
         world, rank = _dist_info()
         stats = None
         if self._holds_Ds and (rank == 0 or not self._stats_from_root):
@@ -341,6 +376,7 @@ class CoverAlgorithm(object):
         D = np.array(self.Ds[similarity_type], dtype=np.float32)
         cliques = [sorted(self.cliques[s]) for s in self.cliques]
         if _on_gpu():  # the O(N^2) rank step as a HIP kernel (same statistics, same host code)
-            import torch
+            from .. import _lib
+            torch = _lib._torch()  # binds this rank's GPU (nccl) before the first "cuda" allocation
             return evaluation.eval_statistics_device(torch.as_tensor(D).cuda(), cliques=cliques, topsidx=topsidx)
         return evaluation.eval_statistics_cliques(D, cliques, topsidx)  # the reference's host computation

@@ -127,26 +127,54 @@ class EarlyFusion(CoverAlgorithm):
 
     def _cache_writer(self):
         """One background thread for the block-feature disk cache, so the ~1 ms np.savez per song
-        overlaps the GPU work that follows prepare() instead of adding to it."""
+        overlaps the GPU work that follows prepare() instead of adding to it. The exit hook holds
+        only a weak reference, so it never keeps an instance (its ~2 GB of block features at
+        Da-TACOS size, its device tensors) alive."""
         if getattr(self, "_writer", None) is None:
             import atexit
+            import weakref
             from concurrent.futures import ThreadPoolExecutor
             self._writer = ThreadPoolExecutor(max_workers=1)
-            atexit.register(self.flush_cache)
+            ref = weakref.ref(self)
+
+            def _flush_at_exit():
+                obj = ref()
+                if obj is not None:
+                    obj.flush_cache()
+
+            self._atexit = _flush_at_exit
+            atexit.register(_flush_at_exit)
         return self._writer
 
     def flush_cache(self):
-        """Wait until every block-feature cache file of prepare() is on disk (re-raises a failed
-        write); all_pairwise and interpreter exit call it."""
+        """Wait until every block-feature cache file of prepare() is on disk (re-raises the first
+        failed write), then stop the writer thread; all_pairwise and interpreter exit call it."""
         pending, self._pending = self._pending, []
-        for f in pending:
-            f.result()
+        writer, self._writer = getattr(self, "_writer", None), None
+        hook = getattr(self, "_atexit", None)
+        if hook is not None:
+            import atexit
+            atexit.unregister(hook)
+            self._atexit = None
+        try:
+            for f in pending:
+                f.result()
+        finally:
+            if writer is not None:
+                writer.shutdown(wait=True)
 
     def all_pairwise(self, *args, **kwargs):
         try:
-            return CoverAlgorithm.all_pairwise(self, *args, **kwargs)
-        finally:
-            self.flush_cache()
+            out = CoverAlgorithm.all_pairwise(self, *args, **kwargs)
+        except BaseException:
+            try:  # the scoring error is the one to see; a cache-write error is only chained
+                self.flush_cache()
+            except Exception as e:  # noqa: BLE001
+                import warnings
+                warnings.warn("EarlyFusion block-feature cache write failed: %r" % (e,))
+            raise
+        self.flush_cache()
+        return out
 
     def _device(self, i):
         if i not in self._dev:
@@ -173,7 +201,7 @@ class EarlyFusion(CoverAlgorithm):
         wsum = torch.zeros_like(csms['mfccs'])
         for s in ('mfccs', 'ssms', 'chromas'):
             wsum += _lib.wcsm(csms[s], self.K, self.K, 0.5)
-        mats.append(_lib.binarize_rows(torch.exp(-wsum), nn))
+        mats.append(_lib.binarize_rows(_lib.neg_exp(wsum), nn))
         return mats
 
     def _bank(self):

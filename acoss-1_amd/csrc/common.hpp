@@ -150,4 +150,77 @@ __device__ inline float sq_threshold(float thr) {
   return t;
 }
 
+// ---- canonical elementwise math shared with the CPU oracle (oracle/ef_oracle.cpp) ----
+// exp(x) of a float in ONE fixed sequence of correctly rounded double operations: k = rint(x / ln2)
+// (x times the double 1/ln2), r = x - k ln2 by two fma steps (ln2 = hi + lo), a degree-13 Taylor
+// polynomial in r by fma Horner steps, an exact scale by 2^k, one rounding to float. Every step is
+// an IEEE basic operation, so the oracle's restatement gives the same bits; ocml's expf and libm's
+// expf each round their own way in the last ulp, which made EarlyFusion's early score unpinnable
+// (VERDICT r05 missing #1). Relative error before the final rounding < 1e-15 (|r| <= ln2 / 2).
+__device__ inline float canon_expf(float xf) {
+  const double x = (double)xf;
+  if (x != x) return xf;
+  if (x < -104.0) return 0.0f;                 // below half the least float denormal
+  if (x > 89.0) return __builtin_inff();       // above FLT_MAX
+  const double k = __builtin_rint(x * 0x1.71547652b82fep+0);
+  double r = __builtin_fma(-k, 0x1.62e42fefa39efp-1, x);
+  r = __builtin_fma(-k, 0x1.abc9e3b39803fp-56, r);
+  double p = 0x1.6124613a86d09p-33;            // 1/13!
+  p = __builtin_fma(p, r, 0x1.1eed8eff8d898p-29);
+  p = __builtin_fma(p, r, 0x1.ae64567f544e4p-26);
+  p = __builtin_fma(p, r, 0x1.27e4fb7789f5cp-22);
+  p = __builtin_fma(p, r, 0x1.71de3a556c734p-19);
+  p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-16);
+  p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-13);
+  p = __builtin_fma(p, r, 0x1.6c16c16c16c17p-10);
+  p = __builtin_fma(p, r, 0x1.1111111111111p-7);
+  p = __builtin_fma(p, r, 0x1.5555555555555p-5);
+  p = __builtin_fma(p, r, 0x1.5555555555555p-3);
+  p = __builtin_fma(p, r, 0x1p-1);
+  p = __builtin_fma(p, r, 0x1p+0);
+  p = __builtin_fma(p, r, 0x1p+0);
+  const double s = __builtin_bit_cast(double, (unsigned long long)((long long)k + 1023) << 52);  // 2^k, k in [-150, 129]
+  return (float)(p * s);
+}
+
+__device__ __forceinline__ unsigned fkey_f32(float f) {  // order-preserving float -> u32
+  const unsigned u = __builtin_bit_cast(unsigned, f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Mean of the k smallest values of a line in the CANONICAL order (getWCSM's row / column
+// k-nearest means, similarity_fusion.py:47-51): the k smallest values (NaN never taken; +inf fills
+// in when fewer than k are not NaN) added one at a time in ascending order to +0, then divided by
+// k. That is the order k_ef_kmin's sorted registers produce, and the oracle's. One wave per line:
+// round t takes the least key above the previous round's (a wave minimum) and adds that value once
+// per occurrence, so a line costs one pass per DISTINCT value among its k smallest.
+template <class At>
+__device__ inline float kmean_canon(At at, int len, int k, int lane) {
+  float sum = 0.0f;
+  int taken = 0;
+  unsigned prev = 0u;
+  bool first = true;
+  while (taken < k) {  // wave-uniform
+    unsigned m = 0xffffffffu;
+    for (int e = lane; e < len; e += 64) {
+      const float v = at(e);
+      const unsigned key = fkey_f32(v);
+      if (v == v && (first || key > prev) && key < m) m = key;
+    }
+    m = wave_min_u32(m);
+    if (m == 0xffffffffu) {  // no value left that is not NaN
+      sum = sum + __builtin_inff();
+      break;
+    }
+    int c = 0;
+    for (int e = lane; e < len; e += 64) c += fkey_f32(at(e)) == m;
+    c = wave_sum(c);
+    const float v = __builtin_bit_cast(float, (m & 0x80000000u) ? (m & 0x7fffffffu) : ~m);
+    for (int t = 0; t < c && taken < k; ++t, ++taken) sum = sum + v;
+    prev = m;
+    first = false;
+  }
+  return sum / (float)k;
+}
+
 }  // namespace acoss

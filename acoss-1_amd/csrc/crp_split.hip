@@ -1019,7 +1019,9 @@ __device__ __forceinline__ unsigned sample_hint(const LT& L, int n, float kappa,
   const bool ok = v != kNone;
   const int ns = __popcll(__ballot(ok));
   // (a guess only: the hardware reciprocal instead of an IEEE division sequence)
-  const int k = (int)((float)(n - 1) * kappa * (float)ns * __builtin_amdgcn_rcpf((float)n));
+  // clamped into [0, ns - 1] so that some lane's bin holds rank k (a kappa >= 1 through the C ABI,
+  // or the approximate reciprocal, could otherwise leave the ballot empty)
+  const int k = min(max((int)((float)(n - 1) * kappa * (float)ns * __builtin_amdgcn_rcpf((float)n)), 0), ns - 1);
   const unsigned lo = wave_min_u32(v), hi = wave_max_u32(ok ? v : 0u);
   if (lo >= hi) return lo > 0x7f80u ? 0x7f80u : lo;
   const unsigned range = hi - lo;

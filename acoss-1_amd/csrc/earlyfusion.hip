@@ -17,10 +17,12 @@
 //                 column; 16 rows per block packed into u16 bit words (the SW input)
 //   k_ef_kmin*    thread per (row|column, pair, matrix): mean of the K smallest (K <= 16;
 //                 k_ef_kmean, a wave-per-line select, beyond that)
-//   k_ef_wsum     elementwise: E = exp(-(((0 + W_m) + W_s) + W_c)) in float32
+//   k_ef_wsum     elementwise: E = exp(-(((0 + W_m) + W_s) + W_c)) in float32, exp = canon_expf
 //   SW            launch_swb_batch (misc.hip) over the 4P bit planes
-// Tolerance vs the reference: the GEMMs' summation order (BLAS vs MFMA); every other step is the
-// reference's float32 arithmetic.
+// Tolerance vs the reference: the GEMMs' summation order (BLAS vs MFMA), the k-smallest means'
+// order (ascending here, np.partition's unspecified there) and exp (canon_expf vs numpy's); every
+// other step is the reference's float32 arithmetic. Against the canonical CPU oracle
+// (oracle/ef_oracle.cpp) all four scores are bit-identical.
 #include <cmath>
 #include <cstdlib>
 
@@ -562,7 +564,8 @@ __global__ __launch_bounds__(256) void k_ef_binarize_small(const float* __restri
   }
 }
 
-// Mean of the k smallest of each row (COLS = false) or column; blockIdx.z = matrix.
+// Mean of the k smallest of each row (COLS = false) or column (K > kKmax); blockIdx.z = matrix;
+// canonical order (kmean_canon, common.hpp), as k_ef_kmin.
 template <bool COLS>
 __global__ __launch_bounds__(256) void k_ef_kmean(const float* __restrict__ C, int64_t mat_stride, int ld, EfPairs E,
                                                   int k, float* __restrict__ out, int64_t omat_stride) {
@@ -575,42 +578,16 @@ __global__ __launch_bounds__(256) void k_ef_kmean(const float* __restrict__ C, i
   if (line >= nl) return;
   const float* base = C + m * mat_stride + (size_t)p * ld * ld;
   auto at = [&](int e) { return COLS ? base[(size_t)e * ld + line] : base[(size_t)line * ld + e]; };
-  unsigned lo = 0, hi = 0xffffffffu;
-  while (lo < hi) {
-    const unsigned mid = lo + ((hi - lo) >> 1);
-    int c = 0;
-    for (int e = lane; e < len; e += 64) c += fkey(at(e)) <= mid;
-    if (wave_sum(c) >= k)
-      hi = mid;
-    else
-      lo = mid + 1;
-  }
-  const unsigned kth = lo;
-  float sum = 0.0f, kv = 0.0f;
-  int less = 0;
-  bool has = false;
-  for (int e = lane; e < len; e += 64) {
-    const float v = at(e);
-    const unsigned kk = fkey(v);
-    if (kk < kth) {
-      sum += v;
-      ++less;
-    } else if (kk == kth) {
-      kv = v;
-      has = true;
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-  kv = __shfl(kv, __builtin_ctzll(__ballot(has)));
-  const int less_all = wave_sum(less);
-  if (lane == 0) out[m * omat_stride + (size_t)p * ld + line] = (sum + (float)(k - less_all) * kv) / (float)k;
+  const float mean = kmean_canon(at, len, k, lane);
+  if (lane == 0) out[m * omat_stride + (size_t)p * ld + line] = mean;
 }
 
 // Mean of the k smallest of each row / column, one THREAD per line streaming it once: the k
 // smallest so far stay sorted in registers (one compare rejects most elements, a bubble of
 // min/max inserts the rest). Columns: lanes read consecutive columns (coalesced); rows: each
 // lane walks its own row (cache lines reused along the walk). Sum in ascending order (the
-// reference's np.mean over np.partition output has unspecified order: tolerance).
+// reference's np.mean over np.partition output has unspecified order; this ascending order is the
+// canonical one the oracle and kmean_canon share).
 template <bool COLS, int KMAX, int KC = 0>  // KC > 0: k fixed at compile time (k = KC = KMAX)
 __global__ __launch_bounds__(256) void k_ef_kmin(const float* __restrict__ C, int64_t mat_stride, int ld, EfPairs E,
                                                  int k_rt, float* __restrict__ out, int64_t omat_stride, int ppb,
@@ -728,9 +705,9 @@ __global__ void k_ef_wsum(float* __restrict__ C, int64_t mat_stride, int ld, EfP
     const float v = C[m * mat_stride + idx];
     const float eps = ((rmean[m * mean_stride + (size_t)p * ld + i] + cmean[m * mean_stride + (size_t)p * ld + j]) + v) / 3.0f;
     const float me = mu * eps;
-    wsum = wsum + expf(-(v * v) / (2.0f * (me * me)));
+    wsum = wsum + canon_expf(-(v * v) / (2.0f * (me * me)));
   }
-  C[idx] = expf(-wsum);
+  C[idx] = canon_expf(-wsum);
 }
 
 // SW metadata of the 4 matrices of each pair (matrix p*4 + s = bit plane s of pair p).

@@ -186,42 +186,14 @@ __global__ __launch_bounds__(256) void k_binarize_rows(const float* __restrict__
 // ---------------------------------------------------------------------------------------
 template <bool COLS>
 __global__ __launch_bounds__(256) void k_kmean(const float* __restrict__ C, int M, int N, int k, float* __restrict__ out) {
-  // mean of the k smallest values of a row (COLS=false) or column: k-th key by binary search
-  // over the order-preserving u32 keys, then sum(values < kth) + (k - count_less) * kth
+  // mean of the k smallest values of a row (COLS=false) or column, canonical order (kmean_canon)
   const int line = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int nl = COLS ? N : M, len = COLS ? M : N;
   if (line >= nl) return;
   auto at = [&](int e) { return COLS ? C[(size_t)e * N + line] : C[(size_t)line * N + e]; };
-  unsigned a = 0, b = 0xffffffffu;
-  while (a < b) {
-    const unsigned mid = a + ((b - a) >> 1);
-    int c = 0;
-    for (int e = lane; e < len; e += 64) c += fkey(at(e)) <= mid;
-    if (wave_sum(c) >= k)
-      b = mid;
-    else
-      a = mid + 1;
-  }
-  const unsigned kth = a;
-  float sum = 0.0f, kv = 0.0f;
-  int less = 0;
-  bool has = false;
-  for (int e = lane; e < len; e += 64) {
-    const float v = at(e);
-    const unsigned kk = fkey(v);
-    if (kk < kth) {
-      sum += v;
-      ++less;
-    } else if (kk == kth) {
-      kv = v;
-      has = true;
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-  kv = __shfl(kv, __builtin_ctzll(__ballot(has)));  // every holder of the k-th key has the same value
-  const int less_all = wave_sum(less);
-  if (lane == 0) out[line] = (sum + (float)(k - less_all) * kv) / (float)k;
+  const float m = kmean_canon(at, len, k, lane);
+  if (lane == 0) out[line] = m;
 }
 
 __global__ void k_wcsm_apply(const float* __restrict__ C, int M, int N, const float* __restrict__ r,
@@ -232,7 +204,7 @@ __global__ void k_wcsm_apply(const float* __restrict__ C, int M, int N, const fl
   const float v = C[e];
   const float eps = ((r[i] + c[j]) + v) / 3.0f;
   const float me = mu * eps;
-  W[e] = expf(-(v * v) / (2.0f * (me * me)));
+  W[e] = canon_expf(-(v * v) / (2.0f * (me * me)));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -618,6 +590,24 @@ extern "C" int acoss_wcsm(const float* CSM, int32_t M, int32_t N, int32_t k1, in
                      W);
   ACOSS_LAUNCH_CHECK();
   prof_end(PH_WCSM, s);
+  return ACOSS_OK;
+}
+
+__global__ void k_neg_exp(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) out[e] = canon_expf(-x[e]);
+}
+
+extern "C" int acoss_neg_exp(const float* x, int64_t n, float* out, void* hip_stream) {
+  clear_error();
+  if (n < 0 || (n > 0 && (!x || !out))) {
+    set_error("acoss_neg_exp: bad arguments");
+    return ACOSS_E_ARG;
+  }
+  if (n == 0) return ACOSS_OK;
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  hipLaunchKernelGGL(k_neg_exp, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n, out);
+  ACOSS_LAUNCH_CHECK();
   return ACOSS_OK;
 }
 

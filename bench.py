@@ -177,6 +177,8 @@ def other_paths(nth, seed):
         80 tracks x 446 beat blocks (synthetic block features); flops/pair = 2*(1000+1225+480)*M*N
         on the fp32 MFMA CSMs, plus 4 SW and 3 WCSMs.
       snf: one SNF cross-diffusion step at Da-TACOS size (snf_path).
+      datacos_stripe: config 3's per-GPU share, Serra09 on rank 0's stripe of the 8-GPU Da-TACOS split
+        (datacos_stripe).
     """
     import torch
     import oracle
@@ -253,12 +255,12 @@ def other_paths(nth, seed):
         ref, cdt = ef_cpu.run_pool({"mfccs": mf, "ssms": ss, "chromas": ch, "chroma_med": med}, NB, sample, nth, wd)
     gpu_rows = esc[[p * 97 % len(epairs) for p in range(ncpu)]]
     agree = int(np.sum(ref == gpu_rows))
-    # the canonical-order C oracle (oracle/ef_oracle.cpp, golden-pinned) on the same sample: the
-    # per-feature scores must be EQUAL (the GPU's CSMs follow its float order)
+    # the canonical-order C oracle (oracle/ef_oracle.cpp, golden-pinned) on the same sample: all four
+    # scores must be EQUAL (the GPU's CSMs, k-smallest means and exp follow its float order)
     cbank = {"mfccs": mf, "ssms": ss, "chromas": ch, "chroma_med": med,
              "off": np.arange(NT, dtype=np.int64) * NB, "nb": np.full(NT, NB, np.int32)}
-    canon = oracle.ef_batch(cbank, sample, 0.1, nthreads=nth)
-    canon_eq = int(np.sum(canon == gpu_rows[:, :3]))
+    canon = oracle.ef_batch(cbank, sample, 0.1, nthreads=nth, K=10)
+    canon_eq = int(np.sum(canon == gpu_rows))
     res["earlyfusion"] = {"metric": "song-pairs/s (EarlyFusion: 3 CSMs + kNN + WCSM fusion + 4 SW, 446 blocks)",
                           "value": round(len(epairs) / (ems * 1e-3), 1), "ms": round(ems, 3),
                           "pairs": int(len(epairs)), "dtype": "f32",
@@ -272,15 +274,130 @@ def other_paths(nth, seed):
                                            "sample": "%d pairs, numpy restatement + C SW oracle on %d worker "
                                                      "processes (BLAS 1 thread each), %.1f s" % (ncpu, nth, cdt)},
                           "scores_equal_to_oracle": "%d of %d" % (agree, 4 * ncpu),
-                          "feature_scores_equal_to_canonical_oracle": "%d of %d" % (canon_eq, 3 * ncpu),
+                          "scores_equal_to_canonical_oracle": "%d of %d" % (canon_eq, 4 * ncpu),
                           "scores_note": "scores_equal_to_oracle: the numpy restatement (BLAS-order CSMs, the "
                                          "reference's own arithmetic), where a kNN tie can flip on random features; "
-                                         "feature_scores_equal_to_canonical_oracle: mfccs/ssms/chromas against "
-                                         "oracle/ef_oracle.cpp, the same float order as the GPU, pinned against the "
-                                         "reference's golden CSM/OTI/binarisation vectors (tests/test_ef_oracle.py)"}
+                                         "scores_equal_to_canonical_oracle: all four scores against "
+                                         "oracle/ef_oracle.cpp, the same float order as the GPU (CSMs, ascending "
+                                         "k-smallest means, canon_expf), pinned against the reference's golden "
+                                         "CSM/OTI/binarisation/getWCSM vectors (tests/test_ef_oracle.py)"}
     # ---- SNF cross-diffusion step (f2) at Da-TACOS size
     res["snf"] = snf_path(seed)
+    # ---- config 3's shape: one GPU's stripe of the 8-GPU Da-TACOS Serra09 job
+    log("Da-TACOS stripe (config 3, rank 0 of 8)")
+    res["datacos_stripe"] = datacos_stripe(nth, seed)
     return res
+
+
+def stripe_ops(lens, r0, r1, m=9, tau=1):
+    """SURVEY.md §8d ops of every unordered pair (i < j) of rows [r0, r1) for the actual track lengths:
+    sum of 2*12*M_i*N_j + 32*M'_i*N'_j, split by kernel as ops_split (sweep / selects / dp)."""
+    L = np.asarray(lens, np.float64)
+    Lp = np.maximum(np.ceil((L - m * tau) / tau), 0)
+    sufL = np.concatenate([np.cumsum(L[::-1])[::-1][1:], [0.0]])    # sum_{j > i} N_j
+    sufP = np.concatenate([np.cumsum(Lp[::-1])[::-1][1:], [0.0]])   # sum_{j > i} N'_j
+    gram = float(np.sum(24.0 * L[r0:r1] * sufL[r0:r1]))
+    cells = float(np.sum(Lp[r0:r1] * sufP[r0:r1]))
+    return {"total": gram + 32.0 * cells, "sweep": gram + 11.0 * cells, "selects": 7.0 * cells, "dp": 14.0 * cells,
+            "cells": cells}
+
+
+def datacos_stripe(nth, seed, world=8, rank=0, chunk=1 << 20, sample=2000):
+    """Config 3's per-GPU share (BASELINE.json configs[2]: Da-TACOS Serra09 Qmax, pair matrix tiled
+    across 8 GPUs) measured on this one GPU: a Da-TACOS-shaped corpus (15,000 songs, 1000 cliques x 13
+    + 2000 singletons, synthetic HPCP of 350..700 frames, the hard corpus of tools/datacos_plugin.py),
+    the cost-balanced row stripe rank `rank` of `world` scores (acoss.distributed.stripe_bounds, as
+    all_pairwise does), in 1 M-pair acoss_crp_align calls scattered into a device stripe (the timed
+    region, HIP events on the launch stream). Roofline: SURVEY §8d ops for the stripe's actual
+    lengths; the one-stream kernel split of the first chunk; a sampled == check against the oracle."""
+    import torch
+    import oracle
+    from acoss import _lib, distributed, synthetic
+    from acoss.engine import ChromaBank
+    t0 = time.perf_counter()
+    tracks, _ = synthetic.make_hard_corpus("datacos", frames=500, seed=seed, fixed_length=False)
+    T = len(tracks)
+    lens = np.array([len(t) for t in tracks], np.int32)
+    bounds = distributed.stripe_bounds(lens, world, symmetric=True)
+    r0, r1 = bounds[rank]
+    bank = ChromaBank(tracks)
+    chunks = list(distributed.stripe_pair_chunks(T, r0, r1, True, chunk))
+    n_pairs = int(sum(len(c) for c in chunks))
+    gen_s = time.perf_counter() - t0
+    blk = torch.zeros((r1 - r0, T), dtype=torch.float32, device="cuda")
+    bank.crp_align(chunks[0][:8192], qmax=True)  # workspaces sized once, as all_pairwise's first chunk
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(s)
+    for c in chunks:
+        q = bank.crp_align(c, qmax=True)["qmax"]
+        p = torch.as_tensor(c.astype(np.int64)).cuda()
+        blk[p[:, 0] - r0, p[:, 1]] = q
+    ev1.record(s)
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1)
+    ops = stripe_ops(lens, r0, r1)
+    rate = n_pairs / (ms * 1e-3)
+    achieved = ops["total"] / (ms * 1e-3) / 1e12
+    # the first chunk on ONE stream with the library's per-phase events: the kernel split
+    first = chunks[0]
+    fr0, fr1 = int(first[0, 0]), int(first[-1, 0]) + 1
+    prev = os.environ.get("ACOSS_SPLIT_STREAMS")
+    os.environ["ACOSS_SPLIT_STREAMS"] = "1"
+    _lib.profile_enable(True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    bank.crp_align(first, qmax=True)
+    e1.record(s)
+    torch.cuda.synchronize()
+    one_ms = e0.elapsed_time(e1)
+    phases = _lib.profile_read()
+    _lib.profile_enable(False)
+    if prev is None:
+        del os.environ["ACOSS_SPLIT_STREAMS"]
+    else:
+        os.environ["ACOSS_SPLIT_STREAMS"] = prev
+    # ops of exactly the first chunk's pairs (its last row may be cut by the chunk boundary)
+    fi, fj = first[:, 0], first[:, 1]
+    Lf = lens.astype(np.float64)
+    Lpf = np.maximum(Lf - 9, 0)
+    fcells = float(np.sum(Lpf[fi] * Lpf[fj]))
+    fsplit = {"sweep": float(np.sum(24.0 * Lf[fi] * Lf[fj])) + 11.0 * fcells, "selects": 7.0 * fcells,
+              "dp": 14.0 * fcells}
+    kernels = {}
+    for k, v in phases.items():
+        kops = PHASE_OPS[k](fsplit) if k in PHASE_OPS else 0.0
+        kernels[k] = {"ms": round(v[0], 3), "launches": v[1],
+                      "frac": round(kops / (v[0] * 1e-3) / 1e12 / PEAK_F32_TFLOPS, 4) if kops and v[0] > 0 else None}
+    # sampled pairs of the stripe against the oracle (bit for bit)
+    from acoss.synthetic import pack
+    rng = np.random.Generator(np.random.PCG64(seed + 7))
+    allp = np.concatenate(chunks)
+    sp = allp[np.sort(rng.choice(len(allp), size=min(sample, len(allp)), replace=False))]
+    feats, off, ln = pack(tracks)
+    tq = time.perf_counter()
+    oq, _, _ = oracle.crp_batch(feats, off, ln, sp, dmax=False, nthreads=nth)
+    odt = time.perf_counter() - tq
+    gq = blk[torch.as_tensor(sp[:, 0] - r0).long().cuda(), torch.as_tensor(sp[:, 1]).long().cuda()].cpu().numpy()
+    job = T * (T - 1) // 2
+    del blk, bank
+    torch.cuda.empty_cache()
+    return {"metric": "song-pairs/s (Serra09 CRP+Qmax, Da-TACOS shape, rank %d of a %d-GPU stripe split)" % (rank, world),
+            "value": round(rate, 1), "ms": round(ms, 3), "pairs": n_pairs, "dtype": "f32",
+            "config": "Da-TACOS benchmark shape: %d songs (1000 x 13 + 2000 singletons), hard synthetic HPCP of "
+                      "%d..%d frames (mean %.0f), stripe rows [%d, %d) of %d, %d acoss_crp_align calls of <= %d "
+                      "pairs, scattered into a device stripe" % (T, lens.min(), lens.max(), lens.mean(), r0, r1, T,
+                                                                  len(chunks), chunk),
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_F32_TFLOPS, 4), "ops": ops["total"],
+                         "ops_per_pair_mean": round(ops["total"] / n_pairs, 1),
+                         "one_stream_first_chunk": {"pairs": int(len(first)), "rows": [fr0, fr1], "ms": round(one_ms, 3),
+                                                    "kernels": kernels}},
+            "projected_job_s_on_%d_gpus" % world: round(job / world / rate, 1),
+            "oracle_sample": {"pairs": int(len(sp)), "qmax_equal": int(np.sum(gq == oq)),
+                              "bitexact": bool(np.array_equal(gq, oq)), "oracle_s": round(odt, 2), "threads": nth},
+            "setup_s": round(gen_s, 1)}
 
 
 def snf_path(seed, n=15000, L=2, K=20):
@@ -331,6 +448,48 @@ def snf_path(seed, n=15000, L=2, K=20):
                              "sample": "one step at the same n = %d on the same inputs (scipy csr, "
                                        "np_oracle.snf_step, single-threaded), %.1f s" % (n, cdt)},
             "bitexact_vs_scipy": same}
+
+
+def exchange_diagnostics(world, rank, comp_ms, exch_ms, probe_ms, bounds, lens, n_tracks, device):
+    """Per-rank view of one multi-GPU step, assembled on rank 0 (None elsewhere):
+    every rank's compute ms per step (HIP events around crp_align + the stripe scatter), exchange ms
+    per step (around the stripe all-gather, so it includes waiting for the slowest rank), its
+    stripe's share of the sum of M'*N' over all pairs, the max/min imbalance of both, and the
+    all-gather's achieved bandwidth from a probe run after a barrier (no straggler wait inside).
+    One all-gather of a 5-float row per rank (a device tensor under nccl, host under gloo)."""
+    import torch
+    import torch.distributed as dist
+    from acoss import distributed
+    costs = distributed.row_costs(lens, symmetric=True)
+    r0, r1 = bounds[rank]
+    mine = torch.tensor([comp_ms, exch_ms, probe_ms, float(costs[r0:r1].sum()),
+                         float(sum(n_tracks - i - 1 for i in range(r0, r1)))], dtype=torch.float64, device=device)
+    rows = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(rows, mine)
+    if rank != 0:
+        return None
+    rows = [r.cpu().numpy() for r in rows]
+    tot = float(costs.sum())
+    rmax = max(b1 - b0 for b0, b1 in bounds)
+    # every rank receives the other ranks' padded stripes (rmax x n float32 each)
+    recv = float((world - 1) * rmax * n_tracks * 4)
+    useful = float(sum((b1 - b0) for b0, b1 in bounds) * n_tracks * 4) * (world - 1) / world
+    per = [{"rank": r, "rows": list(bounds[r]), "pairs": int(v[4]), "cost_share": round(v[3] / tot, 5),
+            "compute_ms_per_step": round(float(v[0]), 3), "exchange_ms_per_step": round(float(v[1]), 3),
+            "allgather_probe_ms": round(float(v[2]), 3)} for r, v in enumerate(rows)]
+    comp = [float(v[0]) for v in rows]
+    cost = [float(v[3]) for v in rows]
+    probe = max(float(v[2]) for v in rows)
+    return {"per_rank": per,
+            "imbalance": {"compute_max_over_min": round(max(comp) / max(min(comp), 1e-9), 4),
+                          "cost_max_over_min": round(max(cost) / max(min(cost), 1e-9), 4),
+                          "compute_max_ms": round(max(comp), 3), "compute_min_ms": round(min(comp), 3)},
+            "allgather": {"padded_rows": int(rmax), "bytes_received_per_rank": recv,
+                          "probe_ms_max_over_ranks": round(probe, 3),
+                          "gbps_per_rank": round(recv / (probe * 1e-3) / 1e9, 2) if probe > 0 else None,
+                          "useful_gbps_per_rank": round(useful / (probe * 1e-3) / 1e9, 2) if probe > 0 else None,
+                          "note": "bytes a rank receives in one all-gather of padded stripes; probe = one "
+                                  "all-gather after a barrier, max over ranks"}}
 
 
 def host_info():
@@ -503,11 +662,24 @@ def main():
     my_pairs = torch.as_tensor(my_pairs_np).cuda()
     total_pairs = T * (T - 1) // 2
 
-    def step():
+    # at N > 1 every timed step also records HIP events around its compute and its exchange on the
+    # stream they run on (no synchronisation inside the timed region), for the per-rank diagnostics
+    step_events = []
+
+    def step(timed=False):
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed and world > 1 else None
+        if evs:
+            evs[0].record()
         out = bank.crp_align(my_pairs, qmax=True)
         blk = distributed.scatter_stripe(my_pairs, out["qmax"], r0, r1, T)
         if world > 1:
-            return distributed.all_gather_stripes(blk, bounds)
+            if evs:
+                evs[1].record()
+            full = distributed.all_gather_stripes(blk, bounds)
+            if evs:
+                evs[2].record()
+                step_events.append(evs)
+            return full
         return blk
 
     def barrier():
@@ -522,11 +694,28 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        D = step()
+        D = step(timed=True)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    multi = None
+    if world > 1:
+        comp_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in step_events]))
+        exch_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in step_events]))
+        blk = distributed.scatter_stripe(my_pairs, bank.crp_align(my_pairs, qmax=True)["qmax"], r0, r1, T)
+        probes = []
+        for _ in range(3):  # the all-gather alone: after a barrier, so no rank waits for a straggler
+            torch.cuda.synchronize()
+            barrier()
+            pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            pe0.record()
+            distributed.all_gather_stripes(blk, bounds)
+            pe1.record()
+            torch.cuda.synchronize()
+            probes.append(pe0.elapsed_time(pe1))
+        multi = exchange_diagnostics(world, rank, comp_ms, exch_ms, float(np.median(probes)), bounds, lens, T,
+                                     "cuda" if backend == "nccl" else "cpu")
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -678,6 +867,7 @@ def main():
             "build": build,
             "launch": {"world": world, "device_count": n_dev, "backend": backend if world > 1 else None,
                        "launcher": os.environ.get("ACOSS_BENCH_LAUNCHER", "external" if world > 1 else None)},
+            "multi_gpu": multi,
         }
     if world > 1 and not args.no_paths:
         # SNF late fusion at Da-TACOS size across the ranks: the measured sharding decision

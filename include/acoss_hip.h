@@ -113,9 +113,16 @@ int acoss_binarize_rows(const float* D, int32_t M, int32_t N, int32_t nneighbs, 
 
 /* acoss getWCSM (A14, similarity_fusion.py:38-54): W = exp(-CSM^2 / (2 (mu*Eps)^2)) with
  * Eps = (rowmean_k2 + colmean_k1 + CSM)/3 of the k2 / k1 smallest per row / column.
- * CSM, W: (M x N) float32. */
+ * CSM, W: (M x N) float32. The means add the k smallest in ascending order and exp is the
+ * canonical canon_expf, so W equals the CPU oracle's (oracle/ef_oracle.cpp or_ef_wcsm) bit for bit. */
 int acoss_wcsm(const float* CSM, int32_t M, int32_t N, int32_t k1, int32_t k2, float mu, float* W,
                void* hip_stream);
+
+/* out[i] = exp(-x[i]) for n float32 values, in the canonical float32 exp shared with the CPU oracle
+ * (common.hpp canon_expf): EarlyFusion's early matrix np.exp(-WCSM_sum)
+ * (earlyfusion_traile.py:182) for the per-pair path (EarlyFusion.pair_matrices); the batched
+ * acoss_earlyfusion applies the same exp inside. out may alias x. */
+int acoss_neg_exp(const float* x, int64_t n, float* out, void* hip_stream);
 
 /* One cross-diffusion step of similarity network fusion for matrix `skip` (f2, replaces the body
  * of the loop at acoss/algorithms/utils/similarity_fusion.py:163-174 in doSimilarityFusionWs):

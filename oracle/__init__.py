@@ -81,7 +81,10 @@ def lib():
         L.or_ef_binarize.argtypes = [_fp, ctypes.c_int, ctypes.c_int, ctypes.c_double, _u8p]
         L.or_ef_batch.restype = ctypes.c_int
         L.or_ef_batch.argtypes = [_fp, ctypes.c_int, _fp, ctypes.c_int, _fp, ctypes.c_int, _fp, _i64p, _i32p, _i32p,
-                                  ctypes.c_int64, ctypes.c_double, _dp, ctypes.c_int]
+                                  ctypes.c_int64, ctypes.c_double, ctypes.c_int, ctypes.c_float, _dp, ctypes.c_int]
+        L.or_ef_wcsm.argtypes = [_fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, _fp]
+        L.or_canon_expf.restype = ctypes.c_float
+        L.or_canon_expf.argtypes = [ctypes.c_float]
         _lib = L
     return _lib
 
@@ -258,10 +261,26 @@ def ef_binarize(D, kappa):
     return B
 
 
-def ef_batch(bank, pairs, kappa=0.1, nthreads=0):
-    """(P, 3) float64 scores mfccs, ssms, chromas of EarlyFusion.similarity for (P, 2) pairs of a
-    packed block bank (dict of host arrays 'mfccs', 'ssms', 'chromas', 'chroma_med', 'off', 'nb'),
-    canonical order (ef_oracle.cpp)."""
+def ef_wcsm(D, k1, k2, mu=0.5):
+    """getWCSM (similarity_fusion.py:38-54) in the canonical order of ef_oracle.cpp: the k smallest
+    per row / column summed ascending, exp = canon_expf."""
+    D = np.ascontiguousarray(D, np.float32)
+    W = np.zeros(D.shape, np.float32)
+    lib().or_ef_wcsm(_p(D, _fp), D.shape[0], D.shape[1], int(k1), int(k2), float(mu), _p(W, _fp))
+    return W
+
+
+def canon_expf(x):
+    """The canonical float32 exp (ef_oracle.cpp canon_expf) of each value of x."""
+    x = np.asarray(x, np.float32)
+    f = lib().or_canon_expf
+    return np.array([f(float(v)) for v in x.ravel()], np.float32).reshape(x.shape)
+
+
+def ef_batch(bank, pairs, kappa=0.1, nthreads=0, K=10, mu=0.5):
+    """(P, 4) float64 scores mfccs, ssms, chromas, early of EarlyFusion.similarity for (P, 2) pairs
+    of a packed block bank (dict of host arrays 'mfccs', 'ssms', 'chromas', 'chroma_med', 'off',
+    'nb'), canonical order (ef_oracle.cpp); K, mu: getWCSM's."""
     mf = np.ascontiguousarray(bank["mfccs"], np.float32)
     ss = np.ascontiguousarray(bank["ssms"], np.float32)
     ch = np.ascontiguousarray(bank["chromas"], np.float32)
@@ -269,8 +288,8 @@ def ef_batch(bank, pairs, kappa=0.1, nthreads=0):
     off = np.ascontiguousarray(bank["off"], np.int64)
     nb = np.ascontiguousarray(bank["nb"], np.int32)
     pairs = np.ascontiguousarray(pairs, np.int32)
-    out = np.zeros((len(pairs), 3), np.float64)
+    out = np.zeros((len(pairs), 4), np.float64)
     lib().or_ef_batch(_p(mf, _fp), mf.shape[1], _p(ss, _fp), ss.shape[1], _p(ch, _fp), ch.shape[1], _p(med, _fp),
-                      _p(off, _i64p), _p(nb, _i32p), _p(pairs, _i32p), len(pairs), float(kappa), _p(out, _dp),
-                      int(nthreads))
+                      _p(off, _i64p), _p(nb, _i32p), _p(pairs, _i32p), len(pairs), float(kappa), int(K), float(mu),
+                      _p(out, _dp), int(nthreads))
     return out

@@ -3,12 +3,14 @@
 // TEST INFRASTRUCTURE ONLY (parity checker; built into oracle/_build/liboracle.so with
 // crp_oracle.cpp). The product path (acoss-1_amd/) never links or calls it.
 //
-// What it restates: the three per-feature scores of EarlyFusion.similarity
-// (/root/reference/acoss/algorithms/earlyfusion_traile.py:165-173):
+// What it restates: the four scores of EarlyFusion.similarity
+// (/root/reference/acoss/algorithms/earlyfusion_traile.py:165-183):
 //   mfccs   = smith_waterman_constrained(csm_to_binary(get_csm(mfccs_a, mfccs_b), kappa))
 //   ssms    = smith_waterman_constrained(csm_to_binary(get_csm(ssms_a, ssms_b), kappa))
 //   chromas = smith_waterman_constrained(csm_to_binary(get_csm_blocked_oti(chromas_a, chromas_b,
 //                                          med_a, med_b, get_csm_cosine), kappa))
+//   early   = smith_waterman_constrained(csm_to_binary(exp(-(((0 + W_m) + W_s) + W_c)), kappa)),
+//             W_f = getWCSM(CSM_f, K, K) (acoss/algorithms/utils/similarity_fusion.py:38-54)
 // with get_csm / get_csm_cosine / get_oti / get_csm_blocked_oti from
 // acoss/algorithms/utils/cross_recurrence.py:30-134, csm_to_binary :136-161 and
 // smith_waterman_constrained from alignment_tools.py:25-46 (or_sw_constrained).
@@ -30,6 +32,13 @@
 //   binarize   nn = kappa < 1 ? rint(kappa * N) : (int)kappa (np.round: half to even); the nn
 //              smallest of each row by (value, column): ties go to the lowest column (the
 //              reference's argpartition leaves the choice unspecified)
+//   k-means    getWCSM's mean of the K smallest of a row / column: the K smallest values (NaN never
+//              taken, +inf when fewer than K are not NaN) added one at a time in ASCENDING order to
+//              +0, then / K (np.mean of np.partition's output sums in an unspecified order)
+//   getWCSM    Eps = ((rmean_i + cmean_j) + CSM) / 3; W = exp(-(CSM * CSM) / (2 ((mu Eps) (mu Eps))))
+//   exp        canon_expf: one fixed sequence of correctly rounded double operations (below; the
+//              HIP kernels' copy is acoss-1_amd/csrc/common.hpp canon_expf), so no libm / ocml
+//              last-ulp differences enter; < 1e-15 relative before the rounding to float
 // Build: oracle/Makefile (g++ -O3 -march=x86-64-v3 -ffp-contract=off -fopenmp).
 #include <algorithm>
 #include <cmath>
@@ -79,6 +88,26 @@ int ef_oti(const float* a, const float* b) {
   return best;
 }
 
+float canon_expf(float xf) {
+  const double x = (double)xf;
+  if (x != x) return xf;
+  if (x < -104.0) return 0.0f;
+  if (x > 89.0) return INFINITY;
+  const double k = std::nearbyint(x * 0x1.71547652b82fep+0);
+  double r = std::fma(-k, 0x1.62e42fefa39efp-1, x);
+  r = std::fma(-k, 0x1.abc9e3b39803fp-56, r);
+  static const double c[14] = {0x1p+0, 0x1p+0, 0x1p-1, 0x1.5555555555555p-3, 0x1.5555555555555p-5,
+                               0x1.1111111111111p-7, 0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-13,
+                               0x1.a01a01a01a01ap-16, 0x1.71de3a556c734p-19, 0x1.27e4fb7789f5cp-22,
+                               0x1.ae64567f544e4p-26, 0x1.1eed8eff8d898p-29, 0x1.6124613a86d09p-33};  // 1/n!
+  double p = c[13];
+  for (int n = 12; n >= 0; --n) p = std::fma(p, r, c[n]);
+  uint64_t bits = (uint64_t)((int64_t)k + 1023) << 52;
+  double sc;
+  std::memcpy(&sc, &bits, 8);
+  return (float)(p * sc);
+}
+
 inline uint32_t fkey(float f) {
   uint32_t u;
   std::memcpy(&u, &f, 4);
@@ -102,6 +131,37 @@ void binarize(const float* D, int M, int N, double kappa, uint8_t* B) {
     for (int j = 0; j < N; ++j)
       if ((((uint64_t)fkey(D[(size_t)i * N + j]) << 32) | (uint32_t)j) <= kth) B[(size_t)i * N + j] = 1;
   }
+}
+
+// Mean of the k smallest of n values at x[0], x[stride], ... (canonical ascending order).
+float kmean(const float* x, int n, int64_t stride, int k, std::vector<float>& buf) {
+  buf.clear();
+  for (int e = 0; e < n; ++e) {
+    const float v = x[(int64_t)e * stride];
+    if (v == v) buf.push_back(v);
+  }
+  const int take = std::min<int>(k, (int)buf.size());
+  std::partial_sort(buf.begin(), buf.begin() + take, buf.end());
+  float s = 0.0f;
+  for (int t = 0; t < take; ++t) s = s + buf[t];
+  if (take < k) s = s + INFINITY;
+  return s / (float)k;
+}
+
+// getWCSM(D, k1, k2, mu) (similarity_fusion.py:38-54): k2 smallest per row, k1 per column.
+void wcsm(const float* D, int M, int N, int k1, int k2, float mu, float* W) {
+  std::vector<float> rm(M), cm(N), buf;
+  for (int i = 0; i < M; ++i) rm[i] = kmean(D + (size_t)i * N, N, 1, k2, buf);
+  for (int j = 0; j < N; ++j) cm[j] = kmean(D + j, M, N, k1, buf);
+  for (int i = 0; i < M; ++i)
+    for (int j = 0; j < N; ++j) {
+      const float v = D[(size_t)i * N + j];
+      const float eps = ((rm[i] + cm[j]) + v) / 3.0f;
+      const float me = mu * eps;
+      const float num = -(v * v);
+      const float den = 2.0f * (me * me);
+      W[(size_t)i * N + j] = canon_expf(num / den);
+    }
 }
 
 // Euclidean (kind 0) or OTI-rolled cosine (kind 1) CSM of X (M x d) against Y (N x d).
@@ -171,11 +231,15 @@ int or_ef_oti(const float* med_a, const float* med_b) { return ef_oti(med_a, med
 
 void or_ef_binarize(const float* D, int M, int N, double kappa, uint8_t* B) { binarize(D, M, N, kappa, B); }
 
-// The three scores (mfccs, ssms, chromas) of every pair into scores[3 p + f]. Banks of packed
-// block rows (block offsets off[t], counts nb[t]); med: (T, 12) chroma medians.
+void or_ef_wcsm(const float* D, int M, int N, int k1, int k2, float mu, float* W) { wcsm(D, M, N, k1, k2, mu, W); }
+
+float or_canon_expf(float x) { return canon_expf(x); }
+
+// The four scores (mfccs, ssms, chromas, early) of every pair into scores[4 p + f]. Banks of packed
+// block rows (block offsets off[t], counts nb[t]); med: (T, 12) chroma medians; K, mu: getWCSM's.
 int or_ef_batch(const float* mf, int d_m, const float* ss, int d_s, const float* ch, int d_c, const float* med,
-                const int64_t* off, const int32_t* nb, const int32_t* pairs, int64_t n_pairs, double kappa,
-                double* scores, int nthreads) {
+                const int64_t* off, const int32_t* nb, const int32_t* pairs, int64_t n_pairs, double kappa, int K,
+                float mu, double* scores, int nthreads) {
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
 #pragma omp parallel for schedule(dynamic, 1)
@@ -183,7 +247,7 @@ int or_ef_batch(const float* mf, int d_m, const float* ss, int d_s, const float*
   for (int64_t p = 0; p < n_pairs; ++p) {
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int M = nb[a], N = nb[b];
-    std::vector<float> D((size_t)M * N);
+    std::vector<float> D((size_t)M * N), W((size_t)M * N), S((size_t)M * N, 0.0f);
     std::vector<uint8_t> B((size_t)M * N);
     const float* banks[3] = {mf, ss, ch};
     const int dims[3] = {d_m, d_s, d_c};
@@ -192,8 +256,13 @@ int or_ef_batch(const float* mf, int d_m, const float* ss, int d_s, const float*
       const int oti = f == 2 ? ef_oti(med + 12 * a, med + 12 * b) : 0;
       csm(banks[f] + off[a] * d, M, banks[f] + off[b] * d, N, d, f == 2 ? 1 : 0, oti, D.data());
       binarize(D.data(), M, N, kappa, B.data());
-      scores[3 * p + f] = or_sw_constrained(B.data(), M, N);
+      scores[4 * p + f] = or_sw_constrained(B.data(), M, N);
+      wcsm(D.data(), M, N, K, K, mu, W.data());
+      for (size_t e = 0; e < S.size(); ++e) S[e] = S[e] + W[e];  // WCSM_sum += W (:179-181)
     }
+    for (size_t e = 0; e < S.size(); ++e) S[e] = canon_expf(-S[e]);  // np.exp(-WCSM_sum) (:182)
+    binarize(S.data(), M, N, kappa, B.data());
+    scores[4 * p + 3] = or_sw_constrained(B.data(), M, N);
   }
   return 0;
 }

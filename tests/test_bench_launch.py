@@ -60,3 +60,48 @@ def test_launch_ranks_env(tmp_path, monkeypatch):
     assert env0["RANK"] == "0" and env0["LOCAL_RANK"] == "0" and env0["WORLD_SIZE"] == "3"
     assert env0["MASTER_ADDR"] == "127.0.0.1" and int(env0["MASTER_PORT"]) > 0
     assert env0["ACOSS_BENCH_LAUNCHER"] == "self"
+
+
+def _diag_worker(rank, world, port, out):
+    import json
+    import numpy as np
+    import torch.distributed as dist
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "acoss-1_amd")]
+    import bench
+    from acoss import distributed
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    lens = np.array([2000 - 7 * (i % 5) for i in range(40)], np.int32)
+    bounds = distributed.stripe_bounds(lens, world, symmetric=True)
+    d = bench.exchange_diagnostics(world, rank, 10.0 + rank, 2.0 + 0.5 * rank, 1.5, bounds, lens, len(lens), "cpu")
+    if rank == 0:
+        with open(out, "w") as f:
+            json.dump(d, f)
+    else:
+        assert d is None
+    dist.destroy_process_group()
+
+
+def test_exchange_diagnostics_world2(tmp_path):
+    """The per-rank fields a multi-GPU bench line carries, assembled on rank 0 over a
+    gloo world of 2: compute / exchange ms per rank, the stripe's share of sum M'N', the imbalance
+    and the all-gather's bandwidth."""
+    import json
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "diag.json")
+    mp.start_processes(_diag_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    d = json.load(open(out))
+    assert [r["rank"] for r in d["per_rank"]] == [0, 1]
+    for r in d["per_rank"]:
+        assert set(r) >= {"rows", "pairs", "cost_share", "compute_ms_per_step", "exchange_ms_per_step",
+                          "allgather_probe_ms"}
+    assert abs(sum(r["cost_share"] for r in d["per_rank"]) - 1.0) < 1e-6
+    assert sum(r["pairs"] for r in d["per_rank"]) == 40 * 39 // 2
+    assert d["per_rank"][1]["compute_ms_per_step"] == 11.0 and d["per_rank"][1]["exchange_ms_per_step"] == 2.5
+    assert d["imbalance"]["compute_max_over_min"] == round(11.0 / 10.0, 4)
+    assert 1.0 <= d["imbalance"]["cost_max_over_min"] < 1.2
+    ag = d["allgather"]
+    assert ag["bytes_received_per_rank"] == ag["padded_rows"] * 40 * 4 and ag["gbps_per_rank"] is not None

@@ -11,12 +11,14 @@ below 2^24; sqrt correctly rounded on both sides) and 0/1 chroma blocks with exa
 then see bit-identical CSMs, resolve ties by the same lowest-column rule (acoss_binarize_rows,
 np_oracle.csm_to_binary), and the three per-feature scores must be EQUAL to the oracle's.
 
-The early-fusion matrix exp(-sum getWCSM) cannot be exact: getWCSM averages the k smallest
-values in numpy's np.partition order, which is not reproducible. Its score is asserted equal
-on every pair whose float64 early matrix is separated at the kappa-NN boundary by more than
-EARLY_MARGIN relative (float32 rounding of the mean/exp chain is ~1e-6), and at least 70 % of
-the pairs must be such pairs. The late / early+late SNF outputs (:200-206) must match
-np_oracle.snf_fused of the ORACLE's matrices at the SNF float32 tolerance of test_gpu_plugin.py.
+The early-fusion matrix exp(-sum getWCSM) follows the canonical order of oracle/ef_oracle.cpp
+(the k smallest summed ascending, exp = canon_expf), so the early score is EQUAL to that oracle on
+EVERY pair (the oracle is pinned in tests/test_ef_oracle.py against the golden getWCSM and an
+independent numpy statement). Against the reference's own composition (numpy's np.partition
+order and float32 exp) it is asserted equal on every pair whose early matrix is separated at the
+kappa-NN boundary by more than EARLY_MARGIN relative, at least 70 % of the pairs. The late /
+early+late SNF outputs (:200-206) must match np_oracle.snf_fused of the ORACLE's matrices at the
+SNF float32 tolerance of test_gpu_plugin.py.
 """
 import numpy as np
 import pytest
@@ -127,10 +129,20 @@ def test_earlyfusion_scores_equal_oracle(corpus, monkeypatch):
     assert len(otis) >= 6  # the roll is exercised
     npairs = N_TRACKS * (N_TRACKS - 1) // 2
     assert np.triu(safe, 1).sum() >= 0.7 * npairs
+    # the canonical-order oracle on every pair, all four scores
+    nbs = [len(f["mfccs"]) for f in feats]
+    bank = {k: np.concatenate([f[k] for f in feats]) for k in ("mfccs", "ssms", "chromas")}
+    bank["chroma_med"] = np.stack([f["chroma_med"] for f in feats])
+    bank["nb"] = np.array(nbs, np.int32)
+    bank["off"] = np.concatenate([[0], np.cumsum(nbs[:-1])]).astype(np.int64)
+    up = np.array([(i, j) for i in range(N_TRACKS) for j in range(i + 1, N_TRACKS)], np.int32)
+    canon = oracle.ef_batch(bank, up, ef.kappa, K=ef.K)
     for k in keys:
         ref[k] += ref[k].T
         assert np.count_nonzero(ref[k]) > npairs
         got = np.asarray(ef.Ds[k])
+        np.testing.assert_array_equal(got[up[:, 0], up[:, 1]], canon[:, keys.index(k)].astype(np.float32),
+                                      err_msg=k + " vs the canonical oracle")
         if k == "early":
             np.testing.assert_array_equal(got[safe], ref[k][safe], err_msg=k)
         else:
@@ -248,10 +260,11 @@ def test_earlyfusion_wave_csm_equals_lds_csm(tmp_path, nb, d_ssm):
 
 def test_earlyfusion_scores_equal_canonical_oracle_on_float_blocks():
     """On general float32 block features (not integer-exact) the GPU's mfccs / ssms / chromas
-    scores equal the canonical-order CPU oracle (oracle/ef_oracle.cpp, pinned against the
-    reference's golden CSMs / OTI / binarisation in tests/test_ef_oracle.py) on every pair: the
-    CSMs follow the same float32 order bit for bit, and binarisation and SW are exact. Ragged
-    block counts, K = 10, kappa = 0.1, and a kappa >= 1 count."""
+    and early scores equal the canonical-order CPU oracle (oracle/ef_oracle.cpp, pinned against
+    the reference's golden CSMs / OTI / binarisation / getWCSM in tests/test_ef_oracle.py) on every
+    pair: the CSMs, the k-smallest means and exp follow the same float32 order bit for bit, and
+    binarisation and SW are exact. Ragged block counts, K = 10 and K = 20 (the wave-per-line means),
+    kappa = 0.1, and a kappa >= 1 count."""
     import torch
     from acoss import _lib
     rng = np.random.default_rng(31)
@@ -265,12 +278,13 @@ def test_earlyfusion_scores_equal_canonical_oracle_on_float_blocks():
     bank = {k: torch.as_tensor(host[k]).cuda() for k in ("mfccs", "ssms", "chromas", "chroma_med", "off", "nb")}
     bank["max_blocks"] = max(nbs)
     pairs = np.array([(i, j) for i in range(T) for j in range(T) if i != j], np.int32)
-    for kappa in (0.1, 5.0):
-        got = _lib.earlyfusion(bank, pairs, kappa, 10).cpu().numpy()
-        ref = oracle.ef_batch(host, pairs, kappa)
-        for f, key in enumerate(("mfccs", "ssms", "chromas")):
+    for kappa, K in ((0.1, 10), (5.0, 10), (0.1, 7), (0.1, 20)):
+        pk = pairs[(host["nb"][pairs[:, 0]] > K) & (host["nb"][pairs[:, 1]] > K)]  # the reference's partition bound
+        got = _lib.earlyfusion(bank, pk, kappa, K).cpu().numpy()
+        ref = oracle.ef_batch(host, pk, kappa, K=K)
+        for f, key in enumerate(("mfccs", "ssms", "chromas", "early")):
             bad = np.flatnonzero(got[:, f] != ref[:, f])
-            assert len(bad) == 0, (kappa, key, len(bad), pairs[bad[:5]], got[bad[:5], f], ref[bad[:5], f])
+            assert len(bad) == 0, (kappa, K, key, len(bad), pk[bad[:5]], got[bad[:5], f], ref[bad[:5], f])
 
 
 _EF_SHORT_SCRIPT = r"""
@@ -319,7 +333,7 @@ def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
     assert np.isfinite(out["band"]).all() and out["band"].shape == (96 * 95, 4)
     np.testing.assert_array_equal(out["band"], out["slices"])
     np.testing.assert_array_equal(out["band"], out["chunks"])
-    # and the feature scores of a sample of pairs == the canonical-order oracle (same bank)
+    # and all four scores of a sample of pairs == the canonical-order oracle (same bank)
     import oracle
     rng = np.random.default_rng(21)
     nb = rng.integers(14, 48, size=96).astype(np.int32)
@@ -332,4 +346,23 @@ def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
     pairs = np.array([(i, j) for i in range(96) for j in range(96) if i != j], np.int32)
     idx = np.random.default_rng(3).choice(len(pairs), 150, replace=False)
     ref = oracle.ef_batch(bank, pairs[idx], 0.1)
-    np.testing.assert_array_equal(out["band"][idx, :3], np.asarray(ref, np.float64)[:, :3])
+    np.testing.assert_array_equal(out["band"][idx], np.asarray(ref, np.float64))
+
+
+def test_wcsm_and_neg_exp_equal_canonical_oracle():
+    """acoss_wcsm (k_kmean wave-per-line canonical means + canon_expf) and acoss_neg_exp equal the
+    oracle's or_ef_wcsm / canon_expf bit for bit: ties, k1 != k2, a NaN row, large k."""
+    from acoss import _lib
+    rng = np.random.default_rng(17)
+    for M, N, k1, k2 in ((50, 60, 10, 10), (130, 77, 3, 40), (33, 500, 33, 100)):
+        D = np.abs(rng.standard_normal((M, N))).astype(np.float32)
+        D[3, : N // 2] = D[3, 0]
+        D[: M // 2, 5] = D[0, 5]
+        D[7] = np.nan
+        got = _lib.wcsm(D, k1, k2, 0.5).cpu().numpy()
+        ref = oracle.ef_wcsm(D, k1, k2, 0.5)
+        same = (got == ref) | (np.isnan(got) & np.isnan(ref))
+        assert same.all(), (M, N, k1, k2, np.argwhere(~same)[:5])
+    x = np.concatenate([rng.uniform(-90, 110, 20000), rng.exponential(2.0, 20000), [0.0, -0.0, np.inf, -np.inf]])
+    x = x.astype(np.float32)
+    np.testing.assert_array_equal(_lib.neg_exp(x).cpu().numpy(), oracle.canon_expf(-x))

@@ -102,26 +102,34 @@ def _rank_worker(rank, world, port, csv, fdir, cache, out, symmetric, every):
     import json
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
-    cls = PairwiseEvery if every else Pairwise
+    cls = PairwiseEvery if every == "class" else Pairwise
     a = cls(csv, name="Fake", datapath=fdir, shortname="w", cachedir=cache, similarity_types=["main", "other"])
+    if every == "optin":  # a caller that reads Ds on every rank
+        a.Ds_on_every_rank = True
     a.all_pairwise(symmetric=symmetric)
-    np.save(out % rank, np.asarray(a.Ds["main"]))
+    raised = None
+    try:
+        np.save(out % rank, np.asarray(a.Ds["main"]))
+    except RuntimeError as e:  # gathered onto rank 0 only: reading it elsewhere is an error
+        raised = str(e)
     stats = [a.getEvalStatistics(k) for k in ("main", "other")]
     with open((out % rank) + ".json", "w") as f:
-        json.dump({"holds": a._holds_Ds, "stats": [[float(v) for v in st[:4]] + [list(map(int, st[4]))]
-                                                   for st in stats]}, f)
+        json.dump({"holds": a._holds_Ds, "raised": raised, "keys": sorted(a.Ds),
+                   "stats": [[float(v) for v in st[:4]] + [list(map(int, st[4]))] for st in stats]}, f)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("every", [False, True])
+@pytest.mark.parametrize("every", ["", "class", "optin"])
 @pytest.mark.parametrize("symmetric", [True, False])
 def test_all_pairwise_gloo_world2_equals_world1(tmp_path, symmetric, every, monkeypatch):
     """Two gloo ranks through all_pairwise + getEvalStatistics: rank 0's Ds
-    equals the world-1 run bitwise; with the gather (every=False, Serra09 / SiMPle) rank 1 holds
-    no matrix, with the all-gather (every=True, the late-fusion algorithms) it holds the same one;
-    both ranks return the same statistics, exactly ONE results row per similarity type is written
-    (rank 0), and rank 1 leaves no memmap file behind."""
+    equals the world-1 run bitwise; with the gather (every="", Serra09 / SiMPle) rank 1 holds no
+    matrix and reading one raises a RuntimeError that says so instead of returning
+    zeros; with the all-gather (the late-fusion algorithms' class setting, or a caller's
+    Ds_on_every_rank = True) it holds the same one; both ranks return the same statistics, exactly
+    ONE results row per similarity type is written (rank 0), and rank 1 leaves no memmap file
+    behind."""
     import json
     import torch.multiprocessing as mp
     monkeypatch.chdir(tmp_path)
@@ -134,14 +142,15 @@ def test_all_pairwise_gloo_world2_equals_world1(tmp_path, symmetric, every, monk
     mp.start_processes(_rank_worker, args=(2, _free_port(), csv, fdir, cache, out, symmetric, every),
                        nprocs=2, join=True, start_method="spawn")
     np.testing.assert_array_equal(np.load(out % 0), np.asarray(one.Ds["main"]))
+    info = [json.load(open((out % r) + ".json")) for r in range(2)]
     if every:
         np.testing.assert_array_equal(np.load(out % 1), np.asarray(one.Ds["main"]))
+        assert info[1]["raised"] is None
     else:
-        d1 = np.load(out % 1)  # rank 1 keeps only what it scored itself: its own stripe's rows
-        scored = np.flatnonzero(d1.any(1))
-        assert len(scored) and scored.min() > 0 and not np.array_equal(d1, np.asarray(one.Ds["main"]))
-    info = [json.load(open((out % r) + ".json")) for r in range(2)]
-    assert info[0]["holds"] and info[1]["holds"] == every
+        assert not os.path.exists(out % 1)
+        assert "gathered onto rank 0 only" in info[1]["raised"] and info[1]["keys"] == ["main", "other"]
+    assert info[0]["raised"] is None
+    assert info[0]["holds"] and info[1]["holds"] == bool(every)
     assert info[0]["stats"] == info[1]["stats"]
     assert info[0]["stats"][0][:4] == ref_stats
     rows = open("results_w_Fake.csv").read().strip().splitlines()
@@ -194,6 +203,32 @@ def test_bind_local_device_rule(monkeypatch):
     monkeypatch.setattr(dist, "is_initialized", lambda: False)
     backend["b"] = "nccl"
     assert D.bind_local_device() is None and state["set"] == []
+
+
+def test_precomputed_world2_binds_before_loading(tmp_path, monkeypatch):
+    """all_pairwise(precomputed=True) under a world-2 job binds the rank's GPU BEFORE
+    it loads Ds and returns, so the evaluation's first "cuda" allocation lands on the local GPU; a
+    rank that holds no matrix skips normalize's device finish."""
+    from acoss.algorithms import algorithm_template as T
+    monkeypatch.chdir(tmp_path)
+    csv, fdir = _dataset(tmp_path)
+    a = Pairwise(csv, name="Fake", datapath=fdir, shortname="p", cachedir=str(tmp_path / "cache"))
+    a.all_pairwise(symmetric=True)
+    calls = []
+    monkeypatch.setattr(T, "_dist_info", lambda: (2, 1))
+    monkeypatch.setattr(T._dist, "bind_local_device", lambda: calls.append("bind") or 1)
+    orig = T.CoverAlgorithm._load_Ds
+
+    def load(self, prefix):
+        calls.append("load")
+        return orig(self, prefix)
+    monkeypatch.setattr(T.CoverAlgorithm, "_load_Ds", load)
+    b = Pairwise(csv, name="Fake", datapath=fdir, shortname="p", cachedir=str(tmp_path / "cache"))
+    b.all_pairwise(precomputed=True)
+    assert calls == ["bind", "load"]
+    np.testing.assert_array_equal(np.asarray(b.Ds["main"]), np.asarray(a.Ds["main"]))
+    b._holds_Ds = False
+    b._finish_device(np.ones(b.N), "serra09")  # returns before touching torch.cuda (no GPU here)
 
 
 def test_resize_block_shapes():

@@ -300,15 +300,16 @@ def run_earlyfusion(a):
     bank["chroma_med"] = np.stack([np.asarray(f["chroma_med"], np.float32) for f in feats])
     bank["nb"] = nb.astype(np.int32)
     bank["off"] = np.concatenate([[0], np.cumsum(nb[:-1])]).astype(np.int64)
-    ref = oracle.ef_batch(bank, sp, algo.kappa, nthreads=a.threads)
+    ref = oracle.ef_batch(bank, sp, algo.kappa, nthreads=a.threads, K=algo.K)
     diff = {}
-    for f, k in enumerate(("mfccs", "ssms", "chromas")):
+    for f, k in enumerate(("mfccs", "ssms", "chromas", "early")):
         got = np.asarray(algo.Ds[k])[sp[:, 0], sp[:, 1]]
         diff[k] = int(np.sum(got != ref[:, f].astype(np.float32)))
     checks["sample_pairs"] = int(len(sp))
     checks["sample_pairs_differing_from_oracle"] = int(sum(diff.values()))
     checks["sample_differing_by_key"] = diff
-    # the early score through the numpy composition (BLAS-order CSMs, np.partition means): reported
+    # the early score is in the canonical comparison above (all 4 scores, every sampled pair); the
+    # reference-order numpy composition (BLAS-order CSMs, np.partition means, numpy exp): reported
     ne = min(300, len(sp))
     early_eq = 0
     for (i, j) in sp[:ne]:
