@@ -29,6 +29,14 @@ class CrpParams(ctypes.Structure):
                 ("oti", ctypes.c_int32), ("gamma_open", ctypes.c_float), ("gamma_ext", ctypes.c_float)]
 
 
+class NpzMember(ctypes.Structure):
+    """acoss_npz_member — one array of an .npz feature file (include/acoss_hip.h)."""
+    _fields_ = [("file", ctypes.c_int32), ("method", ctypes.c_int32), ("ndim", ctypes.c_int32),
+                ("fortran", ctypes.c_int32), ("shape", ctypes.c_int64 * 8), ("nbytes", ctypes.c_int64),
+                ("member_off", ctypes.c_int64), ("comp_size", ctypes.c_int64), ("npy_size", ctypes.c_int64),
+                ("data_skip", ctypes.c_int64), ("name", ctypes.c_char * 128), ("descr", ctypes.c_char * 32)]
+
+
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
@@ -45,6 +53,9 @@ SIGNATURES = {
     "acoss_binarize_rows": [_vp, _i32, _i32, _i32, _vp, _vp],
     "acoss_wcsm": [_vp, _i32, _i32, _i32, _i32, _f32, _vp, _vp],
     "acoss_neg_exp": [_vp, _i64, _vp, _vp],
+    "acoss_npz_index": [ctypes.POINTER(ctypes.c_char_p), _i32, ctypes.c_char_p, _i32, ctypes.POINTER(NpzMember), _i64,
+                        ctypes.POINTER(ctypes.c_int64)],
+    "acoss_npz_read": [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(NpzMember), _i64, ctypes.POINTER(_vp), _i32],
     "acoss_snf_step": [_vp, _i32, _i32, _i32, _vp, _vp, _i32, ctypes.c_double, _vp, _i32, _vp],
     "acoss_snf_diffuse_rows": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i32, _vp],
     "acoss_snf_left_rows": [_vp, _i32, _i32, _i32, _vp, _vp, _i32, ctypes.c_double, _vp, _i32, _vp],
@@ -325,6 +336,45 @@ def wcsm(CSM, k1, k2, mu=0.5):
     out = torch.empty(C.shape, dtype=torch.float32, device="cuda")
     rc = lib.acoss_wcsm(_ptr(C), int(C.shape[0]), int(C.shape[1]), int(k1), int(k2), float(mu), _ptr(out), _stream())
     _check(rc, "acoss_wcsm")
+    return out
+
+
+def npz_read_many(paths, keys=None, n_threads=0):
+    """The arrays of many .npz files, read on native threads in two C calls (acoss_npz_index,
+    acoss_npz_read; host only, no GPU, the GIL released inside both): a list (one per path, in
+    order) of {member name: ndarray}, names as stored ('madmom_features/onsets'). keys: read only
+    members whose top-level name is in keys (None: all). Raises IOError naming the file on an
+    unreadable or unsupported file (object arrays are refused, as np.load(allow_pickle=False))."""
+    lib = load_library()
+    n = len(paths)
+    if n == 0:
+        return []
+    cpaths = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
+    ckeys = None if keys is None else "\n".join(keys).encode()
+    cap = max(16, n * (4 if keys is not None else 8))
+    while True:
+        buf = (NpzMember * cap)()
+        got = ctypes.c_int64(0)
+        rc = lib.acoss_npz_index(cpaths, n, ckeys, int(n_threads), buf, cap, ctypes.byref(got))
+        if rc == ACOSS_OK:
+            break
+        if got.value > cap:
+            cap = int(got.value)
+            continue
+        raise IOError(lib.acoss_last_error().decode(errors="replace"))
+    members = buf[:got.value]
+    out = [dict() for _ in range(n)]
+    arrays = []
+    for m in members:
+        shape = tuple(int(m.shape[d]) for d in range(m.ndim))
+        a = np.empty(shape, dtype=np.dtype(m.descr.decode()), order="F" if m.fortran else "C")
+        arrays.append(a)
+        out[m.file][m.name.decode()] = a
+    if members:
+        dst = (_vp * len(members))(*[a.ctypes.data for a in arrays])
+        rc = lib.acoss_npz_read(cpaths, buf, len(members), dst, int(n_threads))
+        if rc != ACOSS_OK:
+            raise IOError(lib.acoss_last_error().decode(errors="replace"))
     return out
 
 

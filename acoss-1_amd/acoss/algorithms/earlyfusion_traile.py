@@ -255,17 +255,21 @@ class EarlyFusion(CoverAlgorithm):
 
     def prepare(self, chunk=256):
         """Every song's block features: from the memory / disk cache, the rest on the GPU in
-        batches of `chunk` songs."""
+        batches of `chunk` songs. The cached block features and the cached songs' labels are read
+        by the native reader in two batched calls (features_io.load_many), not one np.load per
+        file."""
         if not self._prepared:
-            missing = []
-            for i in range(self.N):
-                if i in self.all_block_feats:
-                    continue
-                try:
-                    self.all_block_feats[i] = _load_feature_file("%s_%i.h5" % (self.get_cacheprefix(), i))
-                    CoverAlgorithm.load_features(self, i)
-                except IOError:
-                    missing.append(i)
+            from ..features_io import cache_readable, load_many
+            todo = [i for i in range(self.N) if i not in self.all_block_feats]
+            paths = {i: "%s_%i.h5" % (self.get_cacheprefix(), i) for i in todo}
+            have = [i for i in todo if cache_readable(paths[i])]
+            if have:
+                for i, bf in zip(have, load_many([paths[i] for i in have])):
+                    self.all_block_feats[i] = bf
+                for i, f in zip(have, load_many([self.filepaths[i] for i in have], keys=("label",))):
+                    self._record_clique(i, f["label"])
+            done = set(have)
+            missing = [i for i in todo if i not in done]
             for c0 in range(0, len(missing), chunk):
                 self._compute_blocks(missing[c0:c0 + chunk])
             self._prepared = True

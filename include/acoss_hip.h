@@ -239,6 +239,38 @@ int acoss_eval_ranks(const float* D, int32_t n, int64_t ld, const int32_t* pos, 
                      const int64_t* m_off, const int32_t* members, int32_t n_queries, int32_t* ranks_out,
                      void* hip_stream);
 
+/* ---------------------------------------------------------------------------------
+ * Per-track feature files (.npz twins of the reference's deepdish .h5 files), read on native
+ * threads: replaces the per-song `dd.io.load` of CoverAlgorithm.load_features
+ * (acoss/algorithms/algorithm_template.py:90) and EarlyFusion.load_features
+ * (acoss/algorithms/earlyfusion_traile.py:88-99) for a whole batch of songs in two calls.
+ * Host only (no GPU); every pointer is a HOST pointer. */
+typedef struct acoss_npz_member {
+  int32_t file;        /* index into paths */
+  int32_t method;      /* zip method: 0 stored (np.savez), 8 deflate (np.savez_compressed) */
+  int32_t ndim;
+  int32_t fortran;     /* fortran_order of the .npy header */
+  int64_t shape[8];
+  int64_t nbytes;      /* bytes of array data (itemsize * prod(shape)) */
+  int64_t member_off;  /* file offset of the member (the .npy stream) */
+  int64_t comp_size;   /* its compressed size */
+  int64_t npy_size;    /* its uncompressed size */
+  int64_t data_skip;   /* offset of the array data inside the .npy stream */
+  char name[128];      /* member name without ".npy", e.g. "madmom_features/onsets" */
+  char descr[32];      /* numpy dtype descr, e.g. "<f4", "<U6" (object dtypes are refused) */
+} acoss_npz_member;
+
+/* Index n_files npz files: every member whose top-level key (the name up to the first '/') is
+ * one of `keys_host` ('\n'-separated; NULL = every member), in file order, then zip order.
+ * *n_out = the member count; ACOSS_E_ARG (message names the file) on an unreadable file or when
+ * the count exceeds max_out (retry with *n_out). n_threads <= 0: every hardware thread. */
+int acoss_npz_index(const char* const* paths_host, int32_t n_files, const char* keys_host, int32_t n_threads,
+                    acoss_npz_member* out_host, int64_t max_out, int64_t* n_out);
+
+/* Read every member's array data into dst_host[i] (nbytes each), one thread per file. */
+int acoss_npz_read(const char* const* paths_host, const acoss_npz_member* members_host, int64_t n_members,
+                   void* const* dst_host, int32_t n_threads);
+
 #ifdef __cplusplus
 }
 #endif
