@@ -463,6 +463,196 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     score[p] = (P % 2) ? dkey_inv(mpk[P / 2]) : 0.5 * (dkey_inv(mpk[P / 2 - 1]) + dkey_inv(mpk[P / 2]));
 }
 
+// ---- MFMA path: L = 10; the frame dots on v_mfma_f64_16x16x4_f64, the windows on the VALU ----
+// A wave owns DW = 64 * KM consecutive diagonals (KM adjacent ones per lane) and walks the rows in
+// blocks of 16 steps. Per block the 16 x (DW + 16) parallelogram of frame dots G(x, y) it needs is
+// computed as DW / 16 + 1 tiles of 16 x 16 by three chained MFMAs each (K = 12 bins in chunks of 4:
+// measured equal to the sequential fma chain, profiles/r05/mfma_probe; the chain starts from -0,
+// so a zero first product keeps its sign exactly as the canonical first product does) and staged
+// in LDS by (step, diagonal); then each step reads its lane's KM dots (one ds_read2_b64), adds them
+// into the open windows (a shift register per diagonal: W[a] = the a most recent dots, so the
+// completed window W[9] + g is the sequential sum in canonical order), and one DPP wave minimum
+// gives the row's minimum, merged into the pair's row-minimum keys by one global atomic per step.
+// What this removes from the VALU: the 12 fma of every dot and the per-step frame hand-over (the
+// K = 4 kernel's 26 DPP moves), about half of its instructions per cell.
+constexpr int kKM = 2;                   // diagonals per lane
+constexpr int kDW = 64 * kKM;            // diagonals per wave
+constexpr int kGT = kDW / 16 + 1;        // 16 x 16 tiles per 16-step block
+constexpr int kGS = kDW + 17;            // LDS row stride in doubles: (kGS - 1) * 2 = 32 mod 64 banks
+typedef double f64x4m __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_simple_mfma(
+    const double* __restrict__ ext, const double* __restrict__ rec, const int32_t* __restrict__ len,
+    const int32_t* __restrict__ pairs, const double* __restrict__ prof, const double* __restrict__ wnorm,
+    const int64_t* __restrict__ toff, int n2max, int64_t n_pairs, int apply_oti, unsigned long long* __restrict__ mpk_g,
+    double* __restrict__ score, int32_t* __restrict__ oti_out) {
+  constexpr int L = kFastL;
+  extern __shared__ double gsm[];  // 4 waves x 16 x kGS doubles; reused for the final sort
+  __shared__ int s_k;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int64_t p = blockIdx.x;
+  if (p >= n_pairs) return;  // whole block
+  const int ta = pairs[2 * p], tb = pairs[2 * p + 1];
+  const int na = len[ta], nb = len[tb];
+  const int P = na - L + 1, Q = nb - L + 1;
+  const bool live = P > 0 && Q > 0;
+  unsigned long long* mpk = mpk_g + (size_t)blockIdx.x * n2max;  // this launch's pair slot
+  if (t == 0) {
+    const int best = simple_oti_index(prof + ta * 12, prof + tb * 12);
+    s_k = apply_oti ? best : 0;
+    if (oti_out) oti_out[p] = best;
+    if (!live) score[p] = __builtin_nan("");
+  }
+  for (int i = t; i < n2max; i += 256) mpk[i] = ~0ull;
+  __threadfence();
+  __syncthreads();
+  if (!live) return;  // whole block (uniform)
+  const int kq = __builtin_amdgcn_readfirstlane(s_k);
+  const int64_t oa = toff[ta], ob0 = toff[tb];
+  const double* Ea = ext + (size_t)oa * kExt + kq;  // query bin (j + kq) mod 12 at offset j
+  const double* Rb = rec + (size_t)ob0 * kRec;
+  const double* Wa = wnorm + oa;
+  const double* Wb = wnorm + ob0;
+  double* G = gsm + (size_t)wave * 16 * kGS;
+  const int ND = P + Q - 1;
+  const int NG = (ND + kDW - 1) / kDW;
+  const double kInf = __builtin_inf();
+  const int li = lane & 15, lk = lane >> 4;  // MFMA operand row / k index
+  for (int g = wave; g < NG; g += 4) {
+    const int ob = -(P - 1) + g * kDW;  // diagonal of lane 0, k = 0
+    const int x_lo = max(0, -(ob + kDW - 1));
+    const int x_hi = min(P - 1, Q - 1 - ob) + L - 1;
+    const int yl = ob + kKM * lane;     // column of diagonal k at step x: x + yl + k
+    double W[kKM][L];                    // W[k][a]: sum of the a most recent dots (a = 1..9)
+#pragma unroll
+    for (int k = 0; k < kKM; ++k)
+#pragma unroll
+      for (int a = 0; a < L; ++a) W[k][a] = 0.0;
+    // MFMA operands of a 16-step block: the query rows (A) and every tile's reference columns (B).
+    // Block b + 1's are loaded while block b's steps run (software pipelined: their latency hides
+    // behind the VALU work of 16 steps).
+    double a0, a1, a2, bv[kGT][3];
+    auto load_ops = [&](int xb) {
+      const double* ar = Ea + (size_t)min(xb + li, na - 1) * kExt + lk;
+      a0 = ar[0];
+      a1 = ar[4];
+      a2 = ar[8];
+#pragma unroll
+      for (int tt = 0; tt < kGT; ++tt) {
+        const int col = min(max(xb + ob + 16 * tt + li, 0), nb - 1);
+        const double* br = Rb + (size_t)col * kRec + lk;
+        bv[tt][0] = br[0];
+        bv[tt][1] = br[4];
+        bv[tt][2] = br[8];
+      }
+    };
+    load_ops(x_lo);
+    for (int x0 = x_lo; x0 <= x_hi; x0 += 16) {
+      // ---- produce: G(x0 + s, x0 + ob + d) for s < 16, d < kDW into LDS [s][d]: the MFMAs, then
+      // branch-free stores (a dot outside the wave's diagonals goes to the row's pad slot kDW,
+      // which no step reads)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // the previous block's reads of G are done
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int tt = 0; tt < kGT; ++tt) {
+        f64x4m acc = {-0.0, -0.0, -0.0, -0.0};
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bv[tt][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bv[tt][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, bv[tt][2], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int s = lk + 4 * r;
+          const int d = 16 * tt + li - s;
+          const int slot = (d >= 0 && d < kDW) ? d : kDW;
+          G[s * kGS + slot] = acc[r];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // ---- consume: 16 steps of windows + row minima, unrolled (static step index) ----
+      const int send = min(16, x_hi - x0 + 1);
+      // the block's reference window norms (columns x0 - 9 + yl + 0..16), then the next block's
+      // MFMA operands (in flight during the 16 steps)
+      const int i0 = x0 - (L - 1) + yl;
+      double sbv[16 + kKM - 1];
+#pragma unroll
+      for (int q = 0; q < 16 + kKM - 1; ++q) {  // clamped loads, then a select: no branch per load
+        const int cc = i0 + q;
+        const double v = Wb[min(max(cc, 0), Q - 1)];
+        sbv[q] = (cc >= 0 && cc < Q) ? v : kInf;
+      }
+      load_ops(x0 + 16);
+      // per step: the lane minimum over its diagonals, written over the step's own G row once the
+      // wave has read it (LDS ops of one wave run in order); after the 16 steps four lanes per row
+      // fold the row's 64 lane minima (16 each, then a quad minimum) -- instead of one dependent
+      // 6-stage DPP wave minimum per step
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        if (s < send) {  // wave-uniform
+          const int r = x0 + s - (L - 1);
+          double gk[kKM];
+#pragma unroll
+          for (int k = 0; k < kKM; ++k) gk[k] = G[s * kGS + kKM * lane + k];
+          const double sar = *(const CDouble*)(Wa + min(max(r, 0), P - 1));
+          double m = kInf;
+#pragma unroll
+          for (int k = 0; k < kKM; ++k) {
+            const double qt = W[k][L - 1] + gk[k];
+            m = vmin_f64(m, fma(-2.0, qt, sbv[s + k] + sar));
+          }
+#pragma unroll
+          for (int k = 0; k < kKM; ++k) {
+#pragma unroll
+            for (int a = L - 1; a >= 2; --a) W[k][a] = W[k][a - 1] + gk[k];
+            W[k][1] = gk[k];
+          }
+          G[s * kGS + lane] = m;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      {
+        const int row = lane >> 2, seg = lane & 3;
+        const double* src = G + row * kGS + 16 * seg;
+        double v = src[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) v = vmin_f64(v, src[i]);
+        v = vmin_f64(v, __shfl_xor(v, 1));
+        v = vmin_f64(v, __shfl_xor(v, 2));
+        const int r = x0 + row - (L - 1);
+        if (seg == 0 && row < send && r >= 0 && r < P && v < kInf) atomicMin(&mpk[r], dkey(v));
+      }
+    }
+  }
+  __threadfence();
+  __syncthreads();  // every wave's atomics complete
+  // the row-minimum keys into LDS, then the bitonic sort and the median as k_simple_diag
+  unsigned long long* sk = reinterpret_cast<unsigned long long*>(gsm);
+  for (int i = t; i < n2max; i += 256) sk[i] = __hip_atomic_load(&mpk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  for (int kk = 2; kk <= n2max; kk <<= 1) {
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < n2max; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long a = sk[i], b = sk[ixj];
+          const bool up = (i & kk) == 0;
+          if ((a > b) == up) {
+            sk[i] = b;
+            sk[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (t == 0) score[p] = (P % 2) ? dkey_inv(sk[P / 2]) : 0.5 * (dkey_inv(sk[P / 2 - 1]) + dkey_inv(sk[P / 2]));
+}
+
 int pow2_at_least(int v) {
   int p = 2;
   while (p < v) p <<= 1;
@@ -561,6 +751,30 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
   const int red = red_kernel ? (renv ? atoi(renv) : (ppb > 1 ? 1 : 0)) : 0;
   const int rboff = ppb * slotsz;
   const size_t lds = ((size_t)rboff + (red ? (size_t)4 * U * kRbufStride : 0)) * 8;
+  // the MFMA kernel (frame dots on v_mfma_f64_16x16x4_f64) with ACOSS_SIMPLE_MFMA=1: bit-identical,
+  // opt-in while it measures slower than the VALU kernels (profiles/r06/simple_mfma/)
+  const char* menv = getenv("ACOSS_SIMPLE_MFMA");
+  const bool mfma = fast && menv && menv[0] == '1';
+  if (mfma) {
+    // one block per pair; the pair's row-minimum keys in a global slot of its own (n2max keys),
+    // so a launch takes at most 256 MB of them
+    const int64_t per = std::max<int64_t>(1, ((int64_t)256 << 20) / ((int64_t)n2max * 8));
+    const size_t mlds = (size_t)4 * 16 * kGS * 8;
+    unsigned long long* mpk_g =
+        static_cast<unsigned long long*>(workspace(16, (size_t)std::min<int64_t>(per, n_pairs) * n2max * 8));
+    if (!mpk_g) return ACOSS_E_HIP;
+    ACOSS_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_simple_mfma),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlds));
+    for (int64_t p0 = 0; p0 < n_pairs; p0 += per) {
+      const int64_t np = std::min<int64_t>(n_pairs - p0, per);
+      hipLaunchKernelGGL(k_simple_mfma, dim3((unsigned)np), dim3(256), mlds, s, ext, rec, track_len, pairs + 2 * p0,
+                         prof, wnorm, toff, n2max, np, apply_oti, mpk_g, score_out + p0,
+                         oti_out ? oti_out + p0 : nullptr);
+      ACOSS_LAUNCH_CHECK();
+    }
+    prof_end(PH_SIMPLE, s);
+    return ACOSS_OK;
+  }
   for (int64_t p0 = 0; p0 < n_pairs; p0 += (int64_t)ppb << 20) {
     const int64_t np = std::min<int64_t>(n_pairs - p0, (int64_t)ppb << 20);
     const int32_t* pp = pairs + 2 * p0;
