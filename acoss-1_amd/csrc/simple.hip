@@ -532,22 +532,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     // MFMA operands of a 16-step block: the query rows (A) and every tile's reference columns (B).
     // Block b + 1's are loaded while block b's steps run (software pipelined: their latency hides
     // behind the VALU work of 16 steps).
+    // Block b + 1's tile t covers block b's tile t + 1 columns (both advance by 16), so a block
+    // shifts the B operands down one tile and loads only its last tile: 3 loads of 64 lanes per
+    // block instead of 27 (the per-tile loads of 16 records each kept the L1 busy).
     double a0, a1, a2, bv[kGT][3];
-    auto load_ops = [&](int xb) {
+    auto load_a = [&](int xb) {
       const double* ar = Ea + (size_t)min(xb + li, na - 1) * kExt + lk;
       a0 = ar[0];
       a1 = ar[4];
       a2 = ar[8];
-#pragma unroll
-      for (int tt = 0; tt < kGT; ++tt) {
-        const int col = min(max(xb + ob + 16 * tt + li, 0), nb - 1);
-        const double* br = Rb + (size_t)col * kRec + lk;
-        bv[tt][0] = br[0];
-        bv[tt][1] = br[4];
-        bv[tt][2] = br[8];
-      }
     };
-    load_ops(x_lo);
+    auto load_b = [&](int xb, int tt) {
+      const int col = min(max(xb + ob + 16 * tt + li, 0), nb - 1);
+      const double* br = Rb + (size_t)col * kRec + lk;
+      bv[tt][0] = br[0];
+      bv[tt][1] = br[4];
+      bv[tt][2] = br[8];
+    };
+    auto load_ops = [&](int xb) {  // the next block's operands (after the current block's MFMAs)
+      load_a(xb);
+#pragma unroll
+      for (int tt = 0; tt < kGT - 1; ++tt)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) bv[tt][c] = bv[tt + 1][c];
+      load_b(xb, kGT - 1);
+    };
+    load_a(x_lo);
+#pragma unroll
+    for (int tt = 0; tt < kGT; ++tt) load_b(x_lo, tt);
     for (int x0 = x_lo; x0 <= x_hi; x0 += 16) {
       // ---- produce: G(x0 + s, x0 + ob + d) for s < 16, d < kDW into LDS [s][d]: the MFMAs, then
       // branch-free stores (a dot outside the wave's diagonals goes to the row's pad slot kDW,
@@ -564,9 +576,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int s = lk + 4 * r;
-          const int d = 16 * tt + li - s;
-          const int slot = (d >= 0 && d < kDW) ? d : kDW;
-          G[s * kGS + slot] = acc[r];
+          const int d = 16 * tt + li - s;  // in [16 tt - 15, 16 tt + 15]: only the end tiles can leave [0, kDW)
+          if (tt == 0 || tt == kGT - 1)
+            G[s * kGS + ((d >= 0 && d < kDW) ? d : kDW)] = acc[r];
+          else
+            G[(kGS - 1) * s + li + 16 * tt] = acc[r];
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -585,29 +599,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         sbv[q] = (cc >= 0 && cc < Q) ? v : kInf;
       }
       load_ops(x0 + 16);
-      // per step: the lane minimum over its diagonals, written over the step's own G row once the
-      // wave has read it (LDS ops of one wave run in order); after the 16 steps four lanes per row
-      // fold the row's 64 lane minima (16 each, then a quad minimum) -- instead of one dependent
-      // 6-stage DPP wave minimum per step
+      // the block's dots of this lane's diagonals, all 16 steps read at once (no LDS latency inside
+      // the steps), and the 16 query window norms (lane s: row x0 + s - 9; read per step by readlane,
+      // so no scalar load shares lgkmcnt with the LDS reads inside the steps)
+      double gall[16][kKM];
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int k = 0; k < kKM; ++k) gall[s][k] = G[s * kGS + kKM * lane + k];
+      const double sa_l = Wa[min(max(x0 + (lane & 15) - (L - 1), 0), P - 1)];
+      // per step: the lane minimum over its diagonals; after the 16 steps the minima go over the G
+      // rows (every read is done) and four lanes per row fold the row's 64 lane minima (16 each,
+      // then a quad minimum) -- instead of one dependent 6-stage DPP wave minimum per step
+      // every step runs (no branch between steps, so the scheduler can overlap them): the steps of
+      // a last block past x_hi read clamped rows, and their minima are dropped below. A step's lane
+      // minimum goes straight over its G row (every read of the block is done: LDS ops of one wave
+      // run in order)
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        if (s < send) {  // wave-uniform
-          const int r = x0 + s - (L - 1);
-          double gk[kKM];
-#pragma unroll
-          for (int k = 0; k < kKM; ++k) gk[k] = G[s * kGS + kKM * lane + k];
-          const double sar = *(const CDouble*)(Wa + min(max(r, 0), P - 1));
+        {
+          const double sar = __builtin_bit_cast(double,
+              ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(__builtin_bit_cast(unsigned long long, sa_l) >> 32), s) << 32) |
+              (unsigned)__builtin_amdgcn_readlane((int)(unsigned)__builtin_bit_cast(unsigned long long, sa_l), s));
           double m = kInf;
 #pragma unroll
           for (int k = 0; k < kKM; ++k) {
-            const double qt = W[k][L - 1] + gk[k];
+            const double qt = W[k][L - 1] + gall[s][k];
             m = vmin_f64(m, fma(-2.0, qt, sbv[s + k] + sar));
           }
 #pragma unroll
           for (int k = 0; k < kKM; ++k) {
 #pragma unroll
-            for (int a = L - 1; a >= 2; --a) W[k][a] = W[k][a - 1] + gk[k];
-            W[k][1] = gk[k];
+            for (int a = L - 1; a >= 2; --a) W[k][a] = W[k][a - 1] + gall[s][k];
+            W[k][1] = gall[s][k];
           }
           G[s * kGS + lane] = m;
         }
@@ -753,8 +777,11 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
   const size_t lds = ((size_t)rboff + (red ? (size_t)4 * U * kRbufStride : 0)) * 8;
   // the MFMA kernel (frame dots on v_mfma_f64_16x16x4_f64) with ACOSS_SIMPLE_MFMA=1: bit-identical,
   // opt-in while it measures slower than the VALU kernels (profiles/r06/simple_mfma/)
+  // default for tracks of >= 256 frames (the VALU kernels pack several short pairs per block:
+  // 200 frames 6.9M vs 4.2M pairs/s; 500 frames 1.22x, 2,000 frames 1.10x for the MFMA kernel,
+  // profiles/r06/simple_mfma/); ACOSS_SIMPLE_MFMA=0 / 1 forces either
   const char* menv = getenv("ACOSS_SIMPLE_MFMA");
-  const bool mfma = fast && menv && menv[0] == '1';
+  const bool mfma = fast && (menv ? menv[0] == '1' : max_len >= 256);
   if (mfma) {
     // one block per pair; the pair's row-minimum keys in a global slot of its own (n2max keys),
     // so a launch takes at most 256 MB of them

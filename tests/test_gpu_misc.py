@@ -190,12 +190,15 @@ def test_simple_batch_vs_oracle(lib):
         assert score[p] == ref or (np.isnan(ref) and np.isnan(score[p]))
 
 
-@pytest.mark.parametrize("sslen,kdiag", [(10, None), (10, "2"), (10, "4"), (10, "5"), (7, None)])
+@pytest.mark.parametrize("sslen,kdiag", [(10, None), (10, "mfma0"), (10, "2"), (10, "4"), (10, "5"), (7, None)])
 def test_simple_long_vs_oracle(lib, monkeypatch, sslen, kdiag):
-    """Fast diagonal kernel (L = 10, K = 2 / 4 / 5 diagonals per lane; K = 4 passes frames by DPP) and the generic sslen path on
+    """The MFMA kernel (the default at these lengths), the VALU diagonal kernels (ACOSS_SIMPLE_MFMA=0;
+    K = 2 / 4 / 5 diagonals per lane, K = 4 passing frames by DPP) and the generic sslen path on
     tracks up to 1300 frames with unequal lengths (ragged diagonal groups), bit-exact."""
     if kdiag is not None:
-        monkeypatch.setenv("ACOSS_SIMPLE_K", kdiag)
+        monkeypatch.setenv("ACOSS_SIMPLE_MFMA", "0")
+        if kdiag != "mfma0":
+            monkeypatch.setenv("ACOSS_SIMPLE_K", kdiag)
     rng = np.random.default_rng(5 + sslen)
     feats = []
     for n in [9, 10, 700, 1300, 513, 96]:
@@ -214,9 +217,12 @@ def test_simple_long_vs_oracle(lib, monkeypatch, sslen, kdiag):
         assert score[p] == ref or (np.isnan(ref) and np.isnan(score[p])), (i, j, score[p], ref)
 
 
-def test_simple_max_length_vs_oracle(lib):
-    """A 4096-frame track (the ABI's maximum: 64 KB of per-pair LDS) against a short one, both
-    directions, plus the short track against itself (zero distances); bit-exact against the oracle."""
+@pytest.mark.parametrize("mfma", ["1", "0"])
+def test_simple_max_length_vs_oracle(lib, monkeypatch, mfma):
+    """A 4096-frame track (the ABI's maximum: 64 KB of per-pair LDS in the VALU kernel, 32 KB of
+    sort keys in the MFMA one) against a short one, both directions, plus the short track against
+    itself (zero distances); bit-exact against the oracle on both kernels."""
+    monkeypatch.setenv("ACOSS_SIMPLE_MFMA", mfma)
     rng = np.random.default_rng(4096)
     feats = []
     for n in [4096, 350]:
@@ -239,6 +245,7 @@ def test_simple_max_length_vs_oracle(lib):
     {"ACOSS_SIMPLE_K": "2", "ACOSS_SIMPLE_RED": "1"},                # LDS row-minimum chunks
     {"ACOSS_SIMPLE_K": "0"},                                         # invalid overrides fall back to the default
     {"ACOSS_SIMPLE_K": "junk", "ACOSS_SIMPLE_PPB": "3"},
+    {"ACOSS_SIMPLE_MFMA": "1"},                                      # the MFMA kernel on short tracks (10..199)
 ])
 def test_simple_kernel_variants_vs_oracle(lib, monkeypatch, env):
     """Every SiMPle kernel variant reachable through the overrides, on short ragged tracks, bit-exact;
