@@ -34,11 +34,11 @@ and checks full-size properties of the result:
   * MAP / MR1 / MRR / MDR / Top-k of the device evaluation (acoss_eval_ranks) equal the host
     restatement of getEvalStatistics on the same matrix;
   * EarlyFusion: the four score matrices symmetric with a zero diagonal and finite; the sampled
-    pairs' mfccs / ssms / chromas scores == the canonical-order CPU oracle (oracle/ef_oracle.cpp,
-    pinned against the reference's golden vectors) on the GPU's block features, which are checked
-    against the numpy restatement (np_oracle.ef_block_features) on a few songs; the early score's
-    agreement with the numpy composition is reported; late / early+late finite; device == host
-    statistics on every key.
+    pairs' mfccs / ssms / chromas / early scores == the canonical-order CPU oracle
+    (oracle/ef_oracle.cpp, pinned against the reference's golden vectors) on the GPU's block
+    features, which are checked against the numpy restatement (np_oracle.ef_block_features) on a
+    few songs; the early score's agreement with the reference-order numpy composition is reported;
+    late / early+late finite; device == host statistics on every key.
 Prints progress, per-stage wall times, peak host RSS, and one JSON line (also written to --out).
 """
 import argparse
