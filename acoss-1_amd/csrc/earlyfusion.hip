@@ -340,6 +340,159 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w(const float* __r
     }
 }
 
+// Short tracks (every track <= 64 blocks: the 32 x 32 tiles of k_ef_csm_w<KIND, 32>), PP pairs per
+// wave. The pairs of a call come in (reference band, query) order, so runs of consecutive pairs
+// share their query track: a wave takes PP consecutive pairs and, when they share it, loads the
+// query rows once for all PP tiles (1 + PP row loads per block instead of 2 PP) and keeps PP
+// independent accumulators in flight. Otherwise (a run boundary) it takes the pairs one at a time.
+// Each output is the same ascending-k fmaf chain as k_ef_csm_w: bit-identical. Used for the cosine
+// chroma CSM (-12 %); the euclid CSMs did not gain (profiles/r06/ef_short_w4/README.txt). Work unit:
+// (group of PP pairs, tile row ti, tile column tj).
+// pairs per wave of the cosine chroma CSM of short tracks. The euclid CSMs (d = 1000, 1228) keep one
+// pair per wave: 2 or 4 pairs sharing the query rows, and a deeper load ring, left them within
+// +-5 % (profiles/r06/ef_short_w4/README.txt); the cosine one (d = 480, 24-k blocks) is 12 % faster
+// with 2 (4: 40 % slower, registers)
+constexpr int kEfPPc = 2;
+
+template <int KIND, int PP>
+__device__ __forceinline__ void ef_csm_w4_tiles(const float* __restrict__ bank, int d, const float* __restrict__ sq,
+                                                const EfPairs& E, const int* __restrict__ oti, int ld, int pbase,
+                                                int npp, int ti, int tj, float* __restrict__ out) {
+  constexpr int KB = KIND == 1 ? 24 : ACOSS_EF_KB, DEPTH = ACOSS_EF_DEPTH, NQ = KB / 8;
+  constexpr int NO = 1 + PP;  // operand rows per lane: the query row, then one reference row per pair
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int a = E.pairs[2 * pbase], M = E.nb[a];
+  const int bi = ti * 32, bj = tj * 32;
+  int bq[PP], Nq[PP];
+  const float* rows[NO];
+  rows[0] = bank + (E.off[a] + min(bi + r, M - 1)) * (int64_t)d + (KB / 2) * h;
+#pragma unroll
+  for (int q = 0; q < PP; ++q) {
+    const int qq = min(q, npp - 1);  // pairs past the group's end repeat its last one (never stored)
+    bq[q] = E.pairs[2 * (pbase + qq) + 1];
+    Nq[q] = E.nb[bq[q]];
+    rows[1 + q] = bank + (E.off[bq[q]] + min(bj + r, Nq[q] - 1)) * (int64_t)d + (KB / 2) * h;
+  }
+  const int nfull = d / KB;
+  f32x4e ring[DEPTH][NO][NQ];
+  auto load = [&](f32x4e (&v)[NO][NQ], int blk) {
+    const int k0 = min(blk, nfull - 1) * KB;
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) v[o][q] = *reinterpret_cast<const f32x4e*>(rows[o] + k0 + 4 * q);
+  };
+  f32x16 acc[PP] = {};
+  int roll[PP];
+#pragma unroll
+  for (int q = 0; q < PP; ++q) roll[q] = KIND == 1 ? __builtin_amdgcn_readfirstlane(oti[pbase + min(q, npp - 1)]) : 0;
+  auto mul = [&](const f32x4e (&vin)[NO][NQ]) {
+    float op[NO][KB / 2];
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+      for (int s2 = 0; s2 < KB / 4; ++s2) {
+        const float lo = vin[o][s2 >> 1][(s2 & 1) * 2], hi = vin[o][s2 >> 1][(s2 & 1) * 2 + 1];
+        const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, lo),
+                                                         __builtin_bit_cast(unsigned, hi), false, false);
+        op[o][s2] = __builtin_bit_cast(float, (unsigned)sw[0]);
+        op[o][s2 + KB / 4] = __builtin_bit_cast(float, (unsigned)sw[1]);
+      }
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {
+      float oq[KB / 2];  // the query operand, rolled by pair q's OTI (cosine)
+#pragma unroll
+      for (int st = 0; st < KB / 2; ++st) oq[st] = op[0][st];
+      if constexpr (KIND == 1) {
+        if (roll[q]) {  // the query row's 12-bin block rotated, as k_ef_csm_w<1> does before the swap
+          float e[12], t[12];
+#pragma unroll
+          for (int c = 0; c < 12; ++c) e[c] = vin[0][c >> 2][c & 3];
+#pragma unroll
+          for (int R = 1; R < 12; ++R)
+            if (roll[q] == R) {
+#pragma unroll
+              for (int c = 0; c < 12; ++c) t[c] = e[(c - R + 12) % 12];
+            }
+#pragma unroll
+          for (int s2 = 0; s2 < KB / 4; ++s2) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, t[2 * s2]),
+                                                             __builtin_bit_cast(unsigned, t[2 * s2 + 1]), false, false);
+            oq[s2] = __builtin_bit_cast(float, (unsigned)sw[0]);
+            oq[s2 + KB / 4] = __builtin_bit_cast(float, (unsigned)sw[1]);
+          }
+        }
+      }
+#pragma unroll
+      for (int st = 0; st < KB / 2; ++st) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(oq[st], op[1 + q][st], acc[q], 0, 0, 0);
+    }
+  };
+  if (nfull > 0) {
+#pragma unroll
+    for (int i = 0; i < DEPTH - 1; ++i) load(ring[i], i);
+#pragma unroll 1
+    for (int kb = 0; kb < nfull; kb += DEPTH) {
+#pragma unroll
+      for (int j = 0; j < DEPTH; ++j) {
+        load(ring[(j + DEPTH - 1) % DEPTH], kb + j + DEPTH - 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (kb + j < nfull) mul(ring[j]);
+      }
+    }
+  }
+  if (d % KB) {
+    const int k0 = nfull * KB;
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        ring[0][o][q] = k0 + (KB / 2) * h + 4 * q < d ? *reinterpret_cast<const f32x4e*>(rows[o] + k0 + 4 * q)
+                                                       : f32x4e{0.0f, 0.0f, 0.0f, 0.0f};
+    mul(ring[0]);
+  }
+#pragma unroll
+  for (int q = 0; q < PP; ++q) {
+    if (q >= npp) break;
+    float* ob = out + (size_t)(pbase + q) * ld * ld;
+    const int col = bj + r;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = bi + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (row < M && col < Nq[q]) {
+        if constexpr (KIND == 1) {
+          ob[(size_t)row * ld + col] = 1.0f - acc[q][reg];
+        } else {
+          float c2 = (sq[E.off[a] + row] + sq[E.off[bq[q]] + col]) - 2.0f * acc[q][reg];
+          if (c2 < 0.0f) c2 = 0.0f;
+          ob[(size_t)row * ld + col] = sqrtf(c2);
+        }
+      }
+    }
+  }
+}
+
+template <int KIND, int PP>
+__global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w4(const float* __restrict__ bank, int d,
+                                                                 const float* __restrict__ sq, EfPairs E,
+                                                                 const int* __restrict__ oti, int ld, int n_pairs,
+                                                                 int n_units, float* __restrict__ out) {
+  const int tiles = (ld + 31) / 32;
+  const int lb = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int unit = lb * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (unit >= n_units) return;
+  const int g = unit / (tiles * tiles), tix = unit - g * tiles * tiles;
+  const int ti = tix / tiles, tj = tix - ti * tiles;
+  const int p0 = g * PP, npp = min(PP, n_pairs - p0);
+  bool same = true;  // wave-uniform: every pair of the group has the group's query track
+  for (int q = 1; q < npp; ++q) same = same && E.pairs[2 * (p0 + q)] == E.pairs[2 * p0];
+  if (same) {
+    if (ti * 32 < E.nb[E.pairs[2 * p0]]) ef_csm_w4_tiles<KIND, PP>(bank, d, sq, E, oti, ld, p0, npp, ti, tj, out);
+    return;
+  }
+  for (int q = 0; q < npp; ++q)  // a run boundary: one pair at a time
+    if (ti * 32 < E.nb[E.pairs[2 * (p0 + q)]]) ef_csm_w4_tiles<KIND, 1>(bank, d, sq, E, oti, ld, p0 + q, 1, ti, tj, out);
+}
+
 // The nn smallest of every row -> 1, ties lowest column (csm_to_binary). A block of 16 waves
 // takes 16 rows (one wave per row) and writes them as one row of u16 bit words (bit r = row
 // 16g + r) in LDS, then to the pair's bit plane for SW. blockIdx.z = CSM plane, written to
@@ -848,6 +1001,9 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   const int kmin_ppb = ld <= 64 ? 4 : 1;
   const unsigned kmin_gx = ld <= 64 ? 1u : (unsigned)((ld + 255) / 256);
   auto kw_cosine = wtile == 32 ? k_ef_csm_w<1, 32> : k_ef_csm_w<1, 64>;
+  // short tracks: the cosine CSM with several consecutive pairs per wave sharing their query rows
+  // (k_ef_csm_w4); ACOSS_EF_W4=0 keeps one pair per wave
+  static const bool w4 = !(getenv("ACOSS_EF_W4") && getenv("ACOSS_EF_W4")[0] == '0');
   int ci = 0;
   for (int64_t p0 = 0; p0 < n_pairs; p0 += chunk, ++ci) {
     const int P = (int)((n_pairs - p0) < chunk ? (n_pairs - p0) : chunk);
@@ -882,7 +1038,11 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
       if (euclid(mfcc, d_mfcc, sq_m, C) != ACOSS_OK || euclid(ssm, d_ssm, sq_s, C + mstride) != ACOSS_OK)
         return ACOSS_E_HIP;
     }
-    if (wave_tiles && d_chroma % 24 == 0)
+    if (wave_tiles && d_chroma % 24 == 0 && w4 && wtile == 32) {
+      const int units = (P + kEfPPc - 1) / kEfPPc * wtiles * wtiles;
+      hipLaunchKernelGGL((k_ef_csm_w4<1, kEfPPc>), dim3((unsigned)((units + 3) / 4)), dim3(256), 0, st, chn, d_chroma,
+                         nullptr, E, oti, ld, P, units, C + 2 * mstride);
+    } else if (wave_tiles && d_chroma % 24 == 0)
       hipLaunchKernelGGL(kw_cosine, dim3((unsigned)((wtiles * wtiles * P + 3) / 4)), dim3(256), 0, st, chn, d_chroma, nullptr, E,
                          oti, ld, wtiles * wtiles * P, C + 2 * mstride);
     else

@@ -312,19 +312,21 @@ np.save(sys.argv[2], out)
 
 
 def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
-    """Da-TACOS-sized tracks (14..47 beat blocks: 32 x 32 CSM tiles, the knockout binarize, one
-    binarize block per matrix, several Smith-Waterman matrices per wave): the scores of one
+    """Da-TACOS-sized tracks (14..47 beat blocks: 32 x 32 CSM tiles with several pairs per wave
+    sharing their query rows, the knockout binarize, one binarize block per matrix, several
+    Smith-Waterman matrices per wave): the scores of one
     9,120-pair call (processed in (reference band, query) order and scattered back) equal those of
-    4,000-pair calls in the caller's order, and those of many small chunks on one stream
-    (ACOSS_EF_BYTES / ACOSS_EF_STREAMS, read once per process, hence separate processes), bit for
-    bit."""
+    4,000-pair calls in the caller's order, those of many small chunks on one stream
+    (ACOSS_EF_BYTES / ACOSS_EF_STREAMS) and those of one pair per CSM wave (ACOSS_EF_W4=0; each read
+    once per process, hence separate processes), bit for bit."""
     import os
     import subprocess
     import sys
     from conftest import ROOT
     out = {}
     for tag, mode, env in (("band", "one", {}), ("slices", "slices", {}),
-                           ("chunks", "one", {"ACOSS_EF_STREAMS": "1", "ACOSS_EF_BYTES": str(8 << 20)})):
+                           ("chunks", "one", {"ACOSS_EF_STREAMS": "1", "ACOSS_EF_BYTES": str(8 << 20)}),
+                           ("w1", "one", {"ACOSS_EF_W4": "0"})):
         f = str(tmp_path / ("%s.npy" % tag))
         r = subprocess.run([sys.executable, "-c", _EF_SHORT_SCRIPT, ROOT, f, mode],
                            env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
@@ -333,6 +335,7 @@ def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
     assert np.isfinite(out["band"]).all() and out["band"].shape == (96 * 95, 4)
     np.testing.assert_array_equal(out["band"], out["slices"])
     np.testing.assert_array_equal(out["band"], out["chunks"])
+    np.testing.assert_array_equal(out["band"], out["w1"])  # several pairs per CSM wave == one pair per wave
     # and all four scores of a sample of pairs == the canonical-order oracle (same bank)
     import oracle
     rng = np.random.default_rng(21)

@@ -6,4 +6,4 @@ cd "$(dirname "$0")/../acoss-1_amd/csrc"
 N=$1; shift
 mkdir -p ../../tools/abl
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -I../../include \
-  -Wno-unused-function -Wno-unused-variable "$@" -o ../../tools/abl/libabl_$N.so *.hip *.cpp
+  -Wno-unused-function -Wno-unused-variable "$@" -o ../../tools/abl/libabl_$N.so *.hip *.cpp -lz
