@@ -683,6 +683,71 @@ __global__ __launch_bounds__(1024) void k_ef_binarize(const float* __restrict__ 
   for (int c = threadIdx.x; c < N; c += 1024) o[c] = (uint16_t)bits[c];
 }
 
+// k_ef_binarize for batches whose tracks all have at most 64 blocks and a small nn (Da-TACOS beat
+// blocks, kappa = 0.1: nn = 1..6): ONE WAVE per (pair, matrix), lane r = row r. The lane loads its
+// row's keys into registers (16-byte loads), then nn rounds each take the row's least key not yet
+// taken (strict <, columns ascending: the lowest column among equal keys, as csm_to_binary's tie
+// rule here); a ballot per column then gives lane c its column's 64-bit row mask, which
+// it writes as the u16 words of the SW bit plane. No LDS, no barrier, no cross-lane reduction per
+// round (k_ef_binarize_small spent 4 waves, two block barriers and a 6-stage wave minimum per round
+// and row). Same selected set as every other binarize kernel.
+__global__ __launch_bounds__(256) void k_ef_binarize_lanes(const float* __restrict__ C, int64_t mat_stride, int ld,
+                                                           EfPairs E, double kappa, uint16_t* __restrict__ Wb,
+                                                           int64_t wplane, int plane0, int nplanes, int n_units) {
+  const int unit = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (unit >= n_units) return;
+  const int p = unit / nplanes, m = unit - p * nplanes;
+  int a, b, M, N;
+  pair_dims(E, p, &a, &b, &M, &N);
+  const int lane = threadIdx.x & 63;
+  const int nn = min(kappa < 1.0 ? (int)rint(kappa * (double)N) : (int)kappa, N);  // as ef_binarize_row
+  unsigned long long sel = 0ull;  // this lane's row: its selected columns
+  if (kappa == 0.0) {
+    sel = N >= 64 ? ~0ull : ((1ull << N) - 1ull);
+  } else if (nn > 0) {
+    const float* xr = C + m * mat_stride + (size_t)p * ld * ld + (size_t)min(lane, M - 1) * ld;
+    unsigned key[64];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (4 * q < N) {  // wave-uniform; ld is a multiple of 4, so the 16-byte load stays in the row
+        const f32x4e v = *reinterpret_cast<const f32x4e*>(xr + 4 * q);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) key[4 * q + u] = 4 * q + u < N ? fkey(v[u]) : 0xffffffffu;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) key[4 * q + u] = 0xffffffffu;
+      }
+    }
+#pragma unroll 1
+    for (int t = 0; t < nn; ++t) {  // wave-uniform; nn <= N, so an untaken column always exists
+      unsigned bk = 0xffffffffu;
+      int bc = -1;
+#pragma unroll
+      for (int c = 0; c < 64; ++c) {
+        if (c < N) {  // wave-uniform
+          const bool better = !((sel >> c) & 1ull) && (bc < 0 || key[c] < bk);
+          bk = better ? key[c] : bk;
+          bc = better ? c : bc;
+        }
+      }
+      sel |= 1ull << bc;
+    }
+  }
+  const unsigned long long rows = M >= 64 ? ~0ull : ((1ull << M) - 1ull);
+  unsigned long long colbits = 0ull;
+#pragma unroll
+  for (int c = 0; c < 64; ++c) {
+    if (c < N) {
+      const unsigned long long bcol = __ballot((sel >> c) & 1ull) & rows;
+      colbits = lane == c ? bcol : colbits;
+    }
+  }
+  const int ng = (M + 15) / 16;
+  uint16_t* o = Wb + ((size_t)p * 4 + plane0 + m) * wplane;
+  if (lane < N)
+    for (int g = 0; g < ng; ++g) o[(size_t)g * ld + lane] = (uint16_t)(colbits >> (16 * g));
+}
+
 // k_ef_binarize for batches whose tracks all have at most 64 blocks (Da-TACOS beat blocks): ONE
 // 256-thread block per (pair, matrix) instead of a 1024-thread block per 16 rows; wave w takes
 // rows w, w + 4, ... with the same per-row selects as k_ef_binarize, into LDS words of 16 rows.
@@ -997,6 +1062,11 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   // one binarize block per (pair, matrix) when every track has at most 64 blocks (15,000 Da-TACOS-
   // shape songs: 4.04M -> 4.38M pairs/s, profiles/r05/ef_short/efbin15k_*.log)
   const bool small_bin = ld <= 64;
+  // ... and one wave per (pair, matrix) with a row per lane when every row's nn is small (the nn
+  // rounds cost nn passes over the row's registers); ACOSS_EF_LANEBIN=0 keeps k_ef_binarize_small
+  const int nn_max = kappa < 1.0 ? (int)rint(kappa * 64.0) : (int)kappa;
+  static const bool lanebin_env = !(getenv("ACOSS_EF_LANEBIN") && getenv("ACOSS_EF_LANEBIN")[0] == '0');
+  const bool lane_bin = small_bin && lanebin_env && nn_max <= 8;
   // column k-smallest means: 4 pairs per 256-thread block when every track has at most 64 blocks
   const int kmin_ppb = ld <= 64 ? 4 : 1;
   const unsigned kmin_gx = ld <= 64 ? 1u : (unsigned)((ld + 255) / 256);
@@ -1051,7 +1121,10 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_CSM, st);
     prof_begin(PH_BIN, st);
-    if (small_bin)
+    if (lane_bin)
+      hipLaunchKernelGGL(k_ef_binarize_lanes, dim3((unsigned)((3 * P + 3) / 4)), dim3(256), 0, st, C, mstride, ld, E,
+                         kappa, Wb, wplane, 0, 3, 3 * P);
+    else if (small_bin)
       hipLaunchKernelGGL(k_ef_binarize_small, dim3(P, 3), dim3(256), 0, st, C, mstride, ld, E, kappa, Wb, wplane, 0);
     else
       hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 3), dim3(1024), bin_lds, st, C, mstride, ld, E, kappa,
@@ -1086,7 +1159,10 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
     ACOSS_LAUNCH_CHECK();
     prof_end(PH_WCSM, st);
     prof_begin(PH_BIN, st);
-    if (small_bin)
+    if (lane_bin)
+      hipLaunchKernelGGL(k_ef_binarize_lanes, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, st, C, mstride, ld, E, kappa,
+                         Wb, wplane, 3, 1, P);
+    else if (small_bin)
       hipLaunchKernelGGL(k_ef_binarize_small, dim3(P, 1), dim3(256), 0, st, C, mstride, ld, E, kappa, Wb, wplane, 3);
     else
       hipLaunchKernelGGL(k_ef_binarize, dim3((ld + 15) / 16, P, 1), dim3(1024), bin_lds, st, C, mstride, ld, E, kappa,

@@ -317,8 +317,9 @@ def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
     Smith-Waterman matrices per wave): the scores of one
     9,120-pair call (processed in (reference band, query) order and scattered back) equal those of
     4,000-pair calls in the caller's order, those of many small chunks on one stream
-    (ACOSS_EF_BYTES / ACOSS_EF_STREAMS) and those of one pair per CSM wave (ACOSS_EF_W4=0; each read
-    once per process, hence separate processes), bit for bit."""
+    (ACOSS_EF_BYTES / ACOSS_EF_STREAMS) and those of one pair per CSM wave and the 4-wave binarize
+    (ACOSS_EF_W4=0, ACOSS_EF_LANEBIN=0; each read once per process, hence separate processes), bit
+    for bit."""
     import os
     import subprocess
     import sys
@@ -326,7 +327,7 @@ def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
     out = {}
     for tag, mode, env in (("band", "one", {}), ("slices", "slices", {}),
                            ("chunks", "one", {"ACOSS_EF_STREAMS": "1", "ACOSS_EF_BYTES": str(8 << 20)}),
-                           ("w1", "one", {"ACOSS_EF_W4": "0"})):
+                           ("w1", "one", {"ACOSS_EF_W4": "0", "ACOSS_EF_LANEBIN": "0"})):
         f = str(tmp_path / ("%s.npy" % tag))
         r = subprocess.run([sys.executable, "-c", _EF_SHORT_SCRIPT, ROOT, f, mode],
                            env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
@@ -335,7 +336,7 @@ def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
     assert np.isfinite(out["band"]).all() and out["band"].shape == (96 * 95, 4)
     np.testing.assert_array_equal(out["band"], out["slices"])
     np.testing.assert_array_equal(out["band"], out["chunks"])
-    np.testing.assert_array_equal(out["band"], out["w1"])  # several pairs per CSM wave == one pair per wave
+    np.testing.assert_array_equal(out["band"], out["w1"])  # the short-track kernels == the one-pair-per-wave ones
     # and all four scores of a sample of pairs == the canonical-order oracle (same bank)
     import oracle
     rng = np.random.default_rng(21)
@@ -369,3 +370,31 @@ def test_wcsm_and_neg_exp_equal_canonical_oracle():
     x = np.concatenate([rng.uniform(-90, 110, 20000), rng.exponential(2.0, 20000), [0.0, -0.0, np.inf, -np.inf]])
     x = x.astype(np.float32)
     np.testing.assert_array_equal(_lib.neg_exp(x).cpu().numpy(), oracle.canon_expf(-x))
+
+
+def test_earlyfusion_short_tracks_ties_equal_canonical_oracle():
+    """Da-TACOS-sized tracks (14..47 beat blocks) with integer-valued block features, so the CSMs are
+    full of exactly equal distances (and whole duplicate blocks: zero distances): the row-per-lane
+    binarize (k_ef_binarize_lanes) must pick the lowest columns among ties as the oracle does. All four
+    scores == the canonical oracle on every ordered pair, for kappa = 0.1 (nn 1..5), 0.2 (nn up to 9:
+    the 4-wave kernel) and a count of 3."""
+    import torch
+    from acoss import _lib
+    rng = np.random.default_rng(77)
+    nbs = [int(v) for v in rng.integers(14, 48, size=20)]
+    R = sum(nbs)
+    host = {"mfccs": rng.integers(-1, 2, size=(R, 1000)).astype(np.float32),
+            "ssms": rng.integers(0, 2, size=(R, 1225)).astype(np.float32),
+            "chromas": rng.integers(0, 3, size=(R, 480)).astype(np.float32),
+            "chroma_med": rng.integers(0, 4, size=(len(nbs), 12)).astype(np.float32),
+            "nb": np.array(nbs, np.int32), "off": np.concatenate([[0], np.cumsum(nbs[:-1])]).astype(np.int64)}
+    host["mfccs"][5] = host["mfccs"][9]  # duplicate blocks: zero distances
+    host["chromas"][5] = host["chromas"][9]
+    bank = {k: torch.as_tensor(host[k]).cuda() for k in ("mfccs", "ssms", "chromas", "chroma_med", "off", "nb")}
+    bank["max_blocks"] = max(nbs)
+    pairs = np.array([(i, j) for i in range(len(nbs)) for j in range(len(nbs)) if i != j], np.int32)
+    for kappa in (0.1, 0.2, 3.0):
+        got = _lib.earlyfusion(bank, pairs, kappa, 10).cpu().numpy()
+        ref = oracle.ef_batch(host, pairs, kappa, K=10)
+        bad = np.argwhere(got != ref)
+        assert len(bad) == 0, (kappa, len(bad), bad[:5])
