@@ -147,6 +147,24 @@ def _check_pairs(pairs, n_tracks):
         raise ValueError("pair indices must lie in [0, %d)" % n_tracks)
 
 
+def _pairs_dev(pairs, n_tracks):
+    """(P, 2) int32 device pairs, bounds-checked. Host (numpy / list) pairs are checked on the
+    host and uploaded from pinned memory without a stream synchronisation, so a caller feeding
+    chunks keeps the GPU busy while it forms the next one; device tensors are checked on the
+    device (two synchronising reductions). Returns (device tensor, host array or None)."""
+    torch = _torch()
+    if isinstance(pairs, torch.Tensor):
+        d = pairs.to(device="cuda", dtype=torch.int32).reshape(-1, 2).contiguous()
+        _check_pairs(d, n_tracks)
+        return d, None
+    h = np.ascontiguousarray(np.asarray(pairs).reshape(-1, 2), dtype=np.int32)
+    if len(h) and (int(h.min()) < 0 or int(h.max()) >= n_tracks):
+        raise ValueError("pair indices must lie in [0, %d)" % n_tracks)
+    if len(h) == 0:
+        return torch.empty((0, 2), dtype=torch.int32, device="cuda"), h
+    return torch.from_numpy(h).pin_memory().to("cuda", non_blocking=True), h
+
+
 def check_knn(J, n):
     """Public form of the kNN index check (see snf_step(validated=True))."""
     _check_knn(J, n)
@@ -181,8 +199,7 @@ def crp_align(feats, track_off, track_len, max_len, pairs, params, qmax=True, dm
     feats = _dev(feats, torch.float32)
     track_off = _dev(track_off, torch.int64)
     track_len = _dev(track_len, torch.int32)
-    pairs = _dev(pairs, torch.int32).reshape(-1, 2)
-    _check_pairs(pairs, int(track_len.shape[0]))
+    pairs, _ = _pairs_dev(pairs, int(track_len.shape[0]))
     P = pairs.shape[0]
     out = {}
     q = torch.empty(P, dtype=torch.float32, device="cuda") if qmax else None
@@ -476,8 +493,7 @@ def simple_mp_packed(flat, track_off, track_len, pairs, sslen=10, apply_oti=True
     torch = _torch()
     lib = load_library()
     lens = np.asarray(track_len.cpu() if isinstance(track_len, torch.Tensor) else track_len, np.int64)
-    pairs = _dev(pairs, torch.int32).reshape(-1, 2)
-    _check_pairs(pairs, len(lens))
+    pairs, _ = _pairs_dev(pairs, len(lens))
     P = pairs.shape[0]
     score = torch.empty(P, dtype=torch.float64, device="cuda")
     oti = torch.empty(P, dtype=torch.int32, device="cuda")
@@ -582,7 +598,10 @@ def _check_ef_neighbours(bank, pairs, kappa, K):
     """Reject pairs whose block counts the reference's argpartition / partition would refuse (see
     ef_neighbour_error) before the kernels run. The smallest counts decide: both conditions are
     monotone in the block count (n - round(kappa n) never decreases with n for kappa < 1)."""
-    nbp = bank["nb"].long()[pairs.long()]
+    if isinstance(pairs, np.ndarray):  # host pairs and the bank's host block counts: no sync
+        nbp = np.asarray(bank["nb_host"])[pairs]
+    else:
+        nbp = bank["nb"].long()[pairs.long()]
     lo_q, lo_r = int(nbp[:, 0].min()), int(nbp[:, 1].min())
     err = ef_neighbour_error([lo_q], [lo_r], kappa, K)
     if err is not None:
@@ -596,13 +615,12 @@ def earlyfusion(bank, pairs, kappa=0.1, K=10, mu=0.5):
     mfccs, ssms, chromas, early."""
     torch = _torch()
     lib = load_library()
-    pairs = _dev(pairs, torch.int32).reshape(-1, 2)
-    _check_pairs(pairs, int(bank["nb"].shape[0]))
+    pairs, host = _pairs_dev(pairs, int(bank["nb"].shape[0]))
     P = pairs.shape[0]
     out = torch.empty((P, 4), dtype=torch.float64, device="cuda")
     if P == 0:
         return out
-    _check_ef_neighbours(bank, pairs, kappa, K)
+    _check_ef_neighbours(bank, pairs if host is None or "nb_host" not in bank else host, kappa, K)
     T = int(bank["nb"].shape[0])
     order = None
     if P > 4096:

@@ -261,7 +261,7 @@ class CoverAlgorithm(object):
         blocks = {k: torch.zeros((r1 - r0, self.N), dtype=torch.float32, device="cuda") for k in self.Ds}
         for chunk in self._pair_chunks(r0, r1, symmetric):
             sc = self._device_scores(chunk)
-            p = torch.as_tensor(np.asarray(chunk, np.int64)).cuda()
+            p = torch.from_numpy(np.ascontiguousarray(chunk, np.int32)).pin_memory().to("cuda", non_blocking=True).long()
             for k in blocks:
                 blocks[k][p[:, 0] - r0, p[:, 1]] = sc[k]
         for k in list(blocks):

@@ -220,7 +220,7 @@ class EarlyFusion(CoverAlgorithm):
             self._dev_bank = {"mfccs": cat("mfccs"), "ssms": cat("ssms"), "chromas": cat("chromas"),
                               "chroma_med": torch.as_tensor(np.stack([np.asarray(f["chroma_med"], np.float32)
                                                                       for f in feats])).cuda(),
-                              "off": torch.as_tensor(off).cuda(), "nb": torch.as_tensor(nb).cuda(),
+                              "off": torch.as_tensor(off).cuda(), "nb": torch.as_tensor(nb).cuda(), "nb_host": nb,
                               "max_blocks": int(nb.max())}
         return self._dev_bank
 

@@ -44,16 +44,19 @@ class ChromaBank:
                   dmax=False, want_oti=False):
         """Serra09 (Qmax) / Chen (dmax) scores for (query, reference) pairs."""
         torch = _lib._torch()
-        pairs = torch.as_tensor(np.asarray(pairs, np.int32)) if not isinstance(pairs, torch.Tensor) else pairs
-        if pairs.numel() == 0:
+        # host pairs stay on the host until _lib.crp_align checks them there and uploads them
+        # without a stream synchronisation (chunk after chunk keeps the GPU busy)
+        pairs = np.asarray(pairs, np.int32).reshape(-1, 2) if not isinstance(pairs, torch.Tensor) else pairs
+        if (pairs.size if isinstance(pairs, np.ndarray) else pairs.numel()) == 0:
             z = torch.zeros(0, dtype=torch.float32, device="cuda")
             return {k: z for k, on in (("qmax", qmax), ("dmax", dmax), ("oti", want_oti)) if on}
         short = []
         if stacked_len(int(self.lens.min()), m, tau) <= 0:  # only then can a pair hold a short track
-            short = [i for i in np.unique(pairs.cpu().numpy()) if stacked_len(self.lens[i], m, tau) <= 0]
+            hp = pairs if isinstance(pairs, np.ndarray) else pairs.cpu().numpy()
+            short = [i for i in np.unique(hp) if stacked_len(self.lens[i], m, tau) <= 0]
         if short:
             raise ValueError("tracks %s are too short for frameStackSize=%d, frameStackStride=%d (essentia raises)"
                              % (short[:5], m, tau))
         params = _lib.crp_params(m, tau, kappa, oti, gamma_open, gamma_ext)
-        return _lib.crp_align(self.feats, self.off, self.len, self.max_len, pairs.cuda(), params, qmax=qmax,
+        return _lib.crp_align(self.feats, self.off, self.len, self.max_len, pairs, params, qmax=qmax,
                               dmax=dmax, oti=want_oti)
