@@ -485,12 +485,185 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_w4(const float* __
   const int p0 = g * PP, npp = min(PP, n_pairs - p0);
   bool same = true;  // wave-uniform: every pair of the group has the group's query track
   for (int q = 1; q < npp; ++q) same = same && E.pairs[2 * (p0 + q)] == E.pairs[2 * p0];
-  if (same) {
-    if (ti * 32 < E.nb[E.pairs[2 * p0]]) ef_csm_w4_tiles<KIND, PP>(bank, d, sq, E, oti, ld, p0, npp, ti, tj, out);
+  // a pair's tile (ti, tj) exists when both tracks reach it; ragged tracks (14..47 blocks at
+  // Da-TACOS lengths) leave many groups where only some pairs reach tile column tj
+  int nv = 0;
+  for (int q = 0; q < npp; ++q)
+    nv += (ti * 32 < E.nb[E.pairs[2 * (p0 + q)]] && tj * 32 < E.nb[E.pairs[2 * (p0 + q) + 1]]) ? 1 : 0;
+  if (same && nv == npp) {
+    ef_csm_w4_tiles<KIND, PP>(bank, d, sq, E, oti, ld, p0, npp, ti, tj, out);
     return;
   }
-  for (int q = 0; q < npp; ++q)  // a run boundary: one pair at a time
-    if (ti * 32 < E.nb[E.pairs[2 * (p0 + q)]]) ef_csm_w4_tiles<KIND, 1>(bank, d, sq, E, oti, ld, p0 + q, 1, ti, tj, out);
+  for (int q = 0; q < npp; ++q)  // a run boundary or a partial group: one pair at a time
+    if (ti * 32 < E.nb[E.pairs[2 * (p0 + q)]] && tj * 32 < E.nb[E.pairs[2 * (p0 + q) + 1]])
+      ef_csm_w4_tiles<KIND, 1>(bank, d, sq, E, oti, ld, p0 + q, 1, ti, tj, out);
+}
+
+// Euclidean CSMs of short tracks (<= 128 blocks) with the reference columns PACKED: the pairs of a
+// call come in (reference band, query) order, so consecutive pairs share their query track; the
+// columns of a run of such pairs (all blocks of every reference track, concatenated) fill
+// 32 NB-wide tiles with no per-pair padding. A tile per pair wastes the part of the tile past the
+// track's block count (14..47 blocks at Da-TACOS lengths: 2.3x the useful MFMA work over rows and
+// columns with 32 x 32 tiles); packing leaves only the rows' padding (1.5x). Lane r of a tile
+// holds NB packed columns, each with its own reference track, block and output pair, so the same
+// 32x32x2 MFMA chains as k_ef_csm_w<0, .> compute every output (bit-identical: the same operands in
+// the same ascending-k fmaf order). Work unit: (group of kEfPack consecutive pairs, row tile ti,
+// packed column tile tc). Within a group the maximal runs of one query track are packed
+// separately; tc counts the runs' tiles in order (at most kEfPack * ceil(ld / 32 NB) of them, so
+// that is the grid's column-tile count).
+// Groups of 64 pairs (one per lane in the walk below): with runs of 32 pairs per query, kernel time
+// per 1M Da-TACOS-shape pairs 209 / 148 / 94 / 87 / 85 ms for groups of 4 / 8 / 16 / 32 / 64, against
+// 119 ms for a 32 x 32 tile per pair (profiles/r06/ef_pack/README.txt)
+#ifndef ACOSS_EF_PACKN
+#define ACOSS_EF_PACKN 64
+#endif
+constexpr int kEfPack = ACOSS_EF_PACKN;
+static_assert(kEfPack <= 64, "one pair per lane");
+
+template <int NB>  // packed columns per wave tile: 32 * NB (NB accumulators sharing the query rows)
+__global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_pack(const float* __restrict__ bank, int d,
+                                                                   const float* __restrict__ sq, EfPairs E, int ld,
+                                                                   int n_pairs, int n_units, float* __restrict__ out) {
+  constexpr int KB = ACOSS_EF_KB, DEPTH = ACOSS_EF_DEPTH, NQ = KB / 8, TW = 32 * NB, NO = 1 + NB;
+  const int wt = (ld + 31) / 32;                // row tiles per track
+  const int ct = kEfPack * ((ld + TW - 1) / TW);  // column-tile slots per group
+  const int lb = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int unit = lb * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (unit >= n_units) return;
+  const int g = unit / (wt * ct), rem = unit - g * wt * ct;
+  const int ti = rem / ct, tc = rem - ti * ct;
+  const int p0 = g * kEfPack, npp = min(kEfPack, n_pairs - p0);
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  // the group's pairs, one per lane (lanes < npp), in two rounds of loads; the walk below reads
+  // them with readlane (a chain of dependent scalar loads here cost more than the tile's MFMAs)
+  int ga = 0, gb = 0;
+  if (lane < npp) {
+    ga = E.pairs[2 * (p0 + lane)];
+    gb = E.pairs[2 * (p0 + lane) + 1];
+  }
+  int gm = 0, gn = 0;
+  int64_t goa = 0, gob = 0;
+  if (lane < npp) {
+    gm = E.nb[ga];
+    gn = E.nb[gb];
+    goa = E.off[ga];
+    gob = E.off[gb];
+  }
+  // find the run (maximal stretch of one query track) holding column tile tc
+  int rs = 0, re = 0, tbase = 0, cols = 0;
+  bool found = false;
+  while (rs < npp) {
+    const int a = __builtin_amdgcn_readlane(ga, rs);
+    re = rs;
+    cols = 0;
+    while (re < npp && __builtin_amdgcn_readlane(ga, re) == a) cols += __builtin_amdgcn_readlane(gn, re), ++re;
+    const int nt = (cols + TW - 1) / TW;
+    if (tc < tbase + nt) {
+      found = true;
+      break;
+    }
+    tbase += nt;
+    rs = re;
+  }
+  if (!found) return;
+  const int M = __builtin_amdgcn_readlane(gm, rs);
+  const int64_t offa = ((int64_t)__builtin_amdgcn_readlane((int)(goa >> 32), rs) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)goa, rs);
+  const int bi = ti * 32;
+  if (bi >= M) return;
+  // this lane's packed columns (one per accumulator): pair q of the run, block c of its reference
+  const float* rows[NO];
+  rows[0] = bank + (offa + min(bi + r, M - 1)) * (int64_t)d + (KB / 2) * h;
+  int cq[NB], cc[NB];
+  int64_t cob[NB];
+  bool cvalid[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int gc = (tc - tbase) * TW + 32 * j + r;
+    cvalid[j] = gc < cols;
+    int q = re - 1, pre = 0, N = 1;
+    int64_t offb = 0;
+    for (int k = rs; k < re; ++k) {  // the last pair of the run takes every column past the others
+      const int n = __builtin_amdgcn_readlane(gn, k);
+      if (gc < pre + n || k == re - 1) {
+        q = k;
+        N = n;
+        offb = ((int64_t)__builtin_amdgcn_readlane((int)(gob >> 32), k) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gob, k);
+        break;
+      }
+      pre += n;
+    }
+    cq[j] = q;
+    cc[j] = min(gc - pre, N - 1);  // clamped for the padding lanes (never stored)
+    cob[j] = offb;
+    rows[1 + j] = bank + (offb + cc[j]) * (int64_t)d + (KB / 2) * h;
+  }
+  const int nfull = d / KB;
+  f32x4e ring[DEPTH][NO][NQ];
+  auto load = [&](f32x4e (&v)[NO][NQ], int blk) {
+    const int k0 = min(blk, nfull - 1) * KB;
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) v[o][qq] = *reinterpret_cast<const f32x4e*>(rows[o] + k0 + 4 * qq);
+  };
+  f32x16 acc[NB] = {};
+  auto mul = [&](const f32x4e (&vin)[NO][NQ]) {
+    float op[NO][KB / 2];
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+      for (int s2 = 0; s2 < KB / 4; ++s2) {
+        const float lo = vin[o][s2 >> 1][(s2 & 1) * 2], hi = vin[o][s2 >> 1][(s2 & 1) * 2 + 1];
+        const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, lo),
+                                                         __builtin_bit_cast(unsigned, hi), false, false);
+        op[o][s2] = __builtin_bit_cast(float, (unsigned)sw[0]);
+        op[o][s2 + KB / 4] = __builtin_bit_cast(float, (unsigned)sw[1]);
+      }
+#pragma unroll
+    for (int st = 0; st < KB / 2; ++st)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[0][st], op[1 + j][st], acc[j], 0, 0, 0);
+  };
+  if (nfull > 0) {
+#pragma unroll
+    for (int i = 0; i < DEPTH - 1; ++i) load(ring[i], i);
+#pragma unroll 1
+    for (int kb = 0; kb < nfull; kb += DEPTH) {
+#pragma unroll
+      for (int j = 0; j < DEPTH; ++j) {
+        load(ring[(j + DEPTH - 1) % DEPTH], kb + j + DEPTH - 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (kb + j < nfull) mul(ring[j]);
+      }
+    }
+  }
+  if (d % KB) {
+    const int k0 = nfull * KB;
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq)
+        ring[0][o][qq] = k0 + (KB / 2) * h + 4 * qq < d ? *reinterpret_cast<const f32x4e*>(rows[o] + k0 + 4 * qq)
+                                                         : f32x4e{0.0f, 0.0f, 0.0f, 0.0f};
+    mul(ring[0]);
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    if (!cvalid[j]) continue;
+    float* ob = out + (size_t)(p0 + cq[j]) * ld * ld + cc[j];
+    const float sqc = sq[cob[j] + cc[j]];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = bi + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (row < M) {
+        float c2 = (sq[offa + row] + sqc) - 2.0f * acc[j][reg];
+        if (c2 < 0.0f) c2 = 0.0f;
+        ob[(size_t)row * ld] = sqrtf(c2);
+      }
+    }
+  }
 }
 
 // The nn smallest of every row -> 1, ties lowest column (csm_to_binary). A block of 16 waves
@@ -1074,6 +1247,12 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   // short tracks: the cosine CSM with several consecutive pairs per wave sharing their query rows
   // (k_ef_csm_w4); ACOSS_EF_W4=0 keeps one pair per wave
   static const bool w4 = !(getenv("ACOSS_EF_W4") && getenv("ACOSS_EF_W4")[0] == '0');
+  // ... and the euclid CSMs with the reference columns of a query's run packed (k_ef_csm_pack):
+  // 32 x 64 tiles (pack_nb = 2) for every track up to 128 blocks; ACOSS_EF_PACK=1 takes 32 x 32
+  // tiles, 0 a tile per pair (Da-TACOS shapes, profiles/r06/ef_pack/README.txt: 14..47 blocks
+  // 4.85M -> 5.72M pairs/s, 30..80 blocks 1.12M -> 1.62M; 32 x 32 tiles 5.68M / 1.59M)
+  static const char* pack_env = getenv("ACOSS_EF_PACK");
+  const int pack_nb = ld > 128 || (pack_env && pack_env[0] == '0') ? 0 : pack_env && pack_env[0] == '1' ? 1 : 2;
   int ci = 0;
   for (int64_t p0 = 0; p0 < n_pairs; p0 += chunk, ++ci) {
     const int P = (int)((n_pairs - p0) < chunk ? (n_pairs - p0) : chunk);
@@ -1097,7 +1276,12 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
           bank = ssm_p;  // the row-padded copy made above
           d = (int)align_up((size_t)d, 4);
         }
-        if (wave_tiles && d % 4 == 0)
+        if (wave_tiles && d % 4 == 0 && pack_nb) {
+          const int tw = 32 * pack_nb;
+          const int units = (P + kEfPack - 1) / kEfPack * ((ld + 31) / 32) * (kEfPack * ((ld + tw - 1) / tw));
+          hipLaunchKernelGGL(pack_nb == 1 ? k_ef_csm_pack<1> : k_ef_csm_pack<2>, dim3((unsigned)((units + 3) / 4)),
+                             dim3(256), 0, st, bank, d, sq, E, ld, P, units, dst);
+        } else if (wave_tiles && d % 4 == 0)
           hipLaunchKernelGGL(kw_euclid, dim3((unsigned)((n_wtiles + 3) / 4)), dim3(256), 0, st, bank, d, sq, E, oti, ld,
                              n_wtiles, dst);
         else

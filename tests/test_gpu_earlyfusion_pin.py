@@ -293,7 +293,8 @@ sys.path[:0] = [sys.argv[1], sys.argv[1] + '/acoss-1_amd']
 from acoss import _lib
 rng = np.random.default_rng(21)
 NT = 96
-nb = rng.integers(14, 48, size=NT).astype(np.int32)  # Da-TACOS beat-block counts
+lo, hi = (int(v) for v in sys.argv[4].split(',')) if len(sys.argv) > 4 else (14, 48)
+nb = rng.integers(lo, hi, size=NT).astype(np.int32)  # Da-TACOS beat-block counts
 off = np.concatenate([[0], np.cumsum(nb[:-1])]).astype(np.int64)
 R = int(nb.sum())
 bank = {'mfccs': torch.as_tensor(rng.standard_normal((R, 1000), dtype=np.float32)).cuda(),
@@ -312,14 +313,14 @@ np.save(sys.argv[2], out)
 
 
 def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
-    """Da-TACOS-sized tracks (14..47 beat blocks: 32 x 32 CSM tiles with several pairs per wave
-    sharing their query rows, the knockout binarize, one binarize block per matrix, several
-    Smith-Waterman matrices per wave): the scores of one
+    """Da-TACOS-sized tracks (14..47 beat blocks: euclid CSM tiles with the reference columns of a
+    query's run packed, cosine 32 x 32 tiles with several pairs per wave sharing their query rows,
+    the row-per-lane binarize, several Smith-Waterman matrices per wave): the scores of one
     9,120-pair call (processed in (reference band, query) order and scattered back) equal those of
     4,000-pair calls in the caller's order, those of many small chunks on one stream
     (ACOSS_EF_BYTES / ACOSS_EF_STREAMS) and those of one pair per CSM wave and the 4-wave binarize
-    (ACOSS_EF_W4=0, ACOSS_EF_LANEBIN=0; each read once per process, hence separate processes), bit
-    for bit."""
+    (ACOSS_EF_W4=0, ACOSS_EF_LANEBIN=0, ACOSS_EF_PACK=0; each read once per process, hence separate
+    processes), bit for bit."""
     import os
     import subprocess
     import sys
@@ -327,7 +328,8 @@ def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
     out = {}
     for tag, mode, env in (("band", "one", {}), ("slices", "slices", {}),
                            ("chunks", "one", {"ACOSS_EF_STREAMS": "1", "ACOSS_EF_BYTES": str(8 << 20)}),
-                           ("w1", "one", {"ACOSS_EF_W4": "0", "ACOSS_EF_LANEBIN": "0"})):
+                           ("w1", "one", {"ACOSS_EF_W4": "0", "ACOSS_EF_LANEBIN": "0", "ACOSS_EF_PACK": "0"}),
+                           ("pack1", "one", {"ACOSS_EF_PACK": "1"})):
         f = str(tmp_path / ("%s.npy" % tag))
         r = subprocess.run([sys.executable, "-c", _EF_SHORT_SCRIPT, ROOT, f, mode],
                            env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
@@ -337,6 +339,7 @@ def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
     np.testing.assert_array_equal(out["band"], out["slices"])
     np.testing.assert_array_equal(out["band"], out["chunks"])
     np.testing.assert_array_equal(out["band"], out["w1"])  # the short-track kernels == the one-pair-per-wave ones
+    np.testing.assert_array_equal(out["band"], out["pack1"])  # 32 x 32 packed tiles
     # and all four scores of a sample of pairs == the canonical-order oracle (same bank)
     import oracle
     rng = np.random.default_rng(21)
@@ -351,6 +354,42 @@ def test_earlyfusion_short_tracks_orders_and_chunks(tmp_path):
     idx = np.random.default_rng(3).choice(len(pairs), 150, replace=False)
     ref = oracle.ef_batch(bank, pairs[idx], 0.1)
     np.testing.assert_array_equal(out["band"][idx], np.asarray(ref, np.float64))
+
+
+def test_earlyfusion_mid_tracks_packed_columns(tmp_path):
+    """30..80 beat blocks (Da-TACOS songs of 350-700 chroma frames): the euclid CSMs with the
+    reference columns packed into 32 x 64 tiles (k_ef_csm_pack<2>, the default up to 128 blocks)
+    equal the 64 x 64 tile per pair (ACOSS_EF_PACK=0) and 32 x 32 packed tiles (ACOSS_EF_PACK=1)
+    bit for bit on all four scores of every
+    ordered pair (one 9,120-pair call in (reference band, query) order, separate processes), and a
+    sample equals the canonical-order oracle."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    out = {}
+    for tag, env in (("pack", {}), ("nopack", {"ACOSS_EF_PACK": "0"}), ("pack1", {"ACOSS_EF_PACK": "1"})):
+        f = str(tmp_path / ("%s.npy" % tag))
+        r = subprocess.run([sys.executable, "-c", _EF_SHORT_SCRIPT, ROOT, f, "one", "30,81"],
+                           env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[tag] = np.load(f)
+    assert np.isfinite(out["pack"]).all()
+    np.testing.assert_array_equal(out["pack"], out["nopack"])
+    np.testing.assert_array_equal(out["pack"], out["pack1"])
+    import oracle
+    rng = np.random.default_rng(21)
+    nb = rng.integers(30, 81, size=96).astype(np.int32)
+    R = int(nb.sum())
+    bank = {"mfccs": rng.standard_normal((R, 1000), dtype=np.float32),
+            "ssms": np.abs(rng.standard_normal((R, 1225), dtype=np.float32)),
+            "chromas": np.abs(rng.standard_normal((R, 480), dtype=np.float32)),
+            "chroma_med": np.abs(rng.standard_normal((96, 12), dtype=np.float32)),
+            "nb": nb, "off": np.concatenate([[0], np.cumsum(nb[:-1])]).astype(np.int64)}
+    pairs = np.array([(i, j) for i in range(96) for j in range(96) if i != j], np.int32)
+    idx = np.random.default_rng(4).choice(len(pairs), 100, replace=False)
+    ref = oracle.ef_batch(bank, pairs[idx], 0.1)
+    np.testing.assert_array_equal(out["pack"][idx], np.asarray(ref, np.float64))
 
 
 def test_wcsm_and_neg_exp_equal_canonical_oracle():

@@ -38,6 +38,8 @@ ap.add_argument("--chunk", type=int, default=1 << 20)
 ap.add_argument("--tracks", type=int, default=15000)
 ap.add_argument("--algo", choices=["serra09", "simple", "earlyfusion"], default="serra09")
 ap.add_argument("--max-pairs", type=int, default=0)
+ap.add_argument("--blocks-lo", type=int, default=0,
+                help="earlyfusion: ragged beat-block counts, uniform in [--blocks-lo, --frames] per track")
 a = ap.parse_args()
 t0 = time.perf_counter()
 rng = np.random.Generator(np.random.PCG64(20250101))
@@ -81,13 +83,18 @@ elif a.algo == "simple":
         return (-sc).float()
 else:
     NB = a.frames
+    nbs = np.full(T, NB, np.int32)
+    if a.blocks_lo:
+        nbs = np.random.Generator(np.random.PCG64(7)).integers(a.blocks_lo, NB + 1, T).astype(np.int32)
+    offs = np.concatenate([[0], np.cumsum(nbs[:-1])]).astype(np.int64)
+    R = int(nbs.sum())
     g = torch.Generator(device="cuda").manual_seed(1)
-    ebank = {"mfccs": torch.randn((T * NB, 1000), device="cuda", generator=g),
-             "ssms": torch.rand((T * NB, 1225), device="cuda", generator=g),
-             "chromas": torch.rand((T * NB, 480), device="cuda", generator=g),
+    ebank = {"mfccs": torch.randn((R, 1000), device="cuda", generator=g),
+             "ssms": torch.rand((R, 1225), device="cuda", generator=g),
+             "chromas": torch.rand((R, 480), device="cuda", generator=g),
              "chroma_med": torch.rand((T, 12), device="cuda", generator=g),
-             "off": torch.as_tensor(np.arange(T, dtype=np.int64) * NB).cuda(),
-             "nb": torch.as_tensor(np.full(T, NB, np.int32)).cuda(), "max_blocks": NB}
+             "off": torch.as_tensor(offs).cuda(), "nb": torch.as_tensor(nbs).cuda(), "nb_host": nbs,
+             "max_blocks": int(nbs.max())}
 
     def score(ch):
         return _lib.earlyfusion(ebank, ch, 0.1, 10)[:, 3].float()
@@ -107,7 +114,9 @@ dt = time.perf_counter() - t1
 job = T * (T - 1) // (2 if symmetric else 1)
 out = {"algo": a.algo, "tracks": T, "frames": a.frames, "world": a.world, "rank": a.rank, "stripe_rows": [r0, r1],
        "pairs": int(len(pairs)), "seconds": round(dt, 2), "pairs_per_s": round(len(pairs) / dt, 1),
-       "job_pairs": job, "projected_job_seconds_on_world": round(job / a.world / (len(pairs) / dt), 1)}
+       "job_pairs": job, "projected_job_seconds_on_world": round(job / a.world / (len(pairs) / dt), 1),
+       "stripe_checksum": float((blk.double() * (torch.arange(blk.numel(), device="cuda", dtype=torch.float64)
+                                                 .reshape(blk.shape) % 7919)).sum())}
 if a.world == 1 and not a.max_pairs and a.algo == "serra09":
     norm = np.sqrt(lens.astype(np.float64))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
