@@ -624,13 +624,23 @@ def earlyfusion(bank, pairs, kappa=0.1, K=10, mu=0.5):
     T = int(bank["nb"].shape[0])
     order = None
     if P > 4096:
-        # pairs in (reference band, query) order: a band of 32 reference tracks' block rows stays
+        # pairs in (reference band, query) order: a band of 16 reference tracks' block rows stays
         # cache-resident while every query track's rows stream past it once per band (an i-major
         # pair list streams every reference track's rows once per query). Scores go back to the
         # caller's order. Da-TACOS shape, 15,000 songs: 3.29M -> 4.07M pairs/s (bands of 16..128
-        # alike; profiles/r05/ef_short/efband15k_*.log).
-        key = (pairs[:, 1].to(torch.int64) // 32) * T + pairs[:, 0].to(torch.int64)
+        # alike; profiles/r05/ef_short/efband15k_*.log). The runs holding the whole band come
+        # first, so they start at multiples of 16 and the CSM kernel's groups of 64 pairs hold
+        # four queries with the same 16 references (k_ef_csm_pack packs their rows and columns;
+        # profiles/r06/ef_pack/README.txt). No host synchronisation: run lengths by scatter_add.
+        band = 16
+        key = (pairs[:, 1].to(torch.int64) // band) * T + pairs[:, 0].to(torch.int64)
         order = torch.argsort(key, stable=True)
+        ks = key[order]
+        start = torch.ones(P, dtype=torch.bool, device=ks.device)
+        start[1:] = ks[1:] != ks[:-1]
+        rid = torch.cumsum(start, 0) - 1
+        runlen = torch.zeros(P, dtype=torch.int64, device=ks.device).scatter_add_(0, rid, torch.ones_like(rid))[rid]
+        order = order[torch.argsort((runlen < band).to(torch.int8), stable=True)]
         pairs = pairs[order].contiguous()
     dst = out if order is None else torch.empty_like(out)
     rc = lib.acoss_earlyfusion(_ptr(bank["mfccs"]), _ptr(bank["ssms"]), _ptr(bank["chromas"]), _ptr(bank["chroma_med"]),

@@ -521,7 +521,7 @@ constexpr int kEfPack = ACOSS_EF_PACKN;
 static_assert(kEfPack <= 64, "one pair per lane");
 
 template <int NB>  // packed columns per wave tile: 32 * NB (NB accumulators sharing the query rows)
-__global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_pack(const float* __restrict__ bank, int d,
+__global__ __launch_bounds__(256, 4) void k_ef_csm_pack(const float* __restrict__ bank, int d,
                                                                    const float* __restrict__ sq, EfPairs E, int ld,
                                                                    int n_pairs, int n_units, float* __restrict__ out) {
   constexpr int KB = ACOSS_EF_KB, DEPTH = ACOSS_EF_DEPTH, NQ = KB / 8, TW = 32 * NB, NO = 1 + NB;
@@ -530,8 +530,7 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_pack(const float* 
   const int lb = xcd_remap((int)blockIdx.x, (int)gridDim.x);
   const int unit = lb * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (unit >= n_units) return;
-  const int g = unit / (wt * ct), rem = unit - g * wt * ct;
-  const int ti = rem / ct, tc = rem - ti * ct;
+  const int g = unit / (wt * ct), u = unit - g * wt * ct;
   const int p0 = g * kEfPack, npp = min(kEfPack, n_pairs - p0);
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   // the group's pairs, one per lane (lanes < npp), in two rounds of loads; the walk below reads
@@ -549,53 +548,103 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_pack(const float* 
     goa = E.off[ga];
     gob = E.off[gb];
   }
-  // find the run (maximal stretch of one query track) holding column tile tc
-  int rs = 0, re = 0, tbase = 0, cols = 0;
+  auto rl64 = [](int64_t v, int l) {
+    return ((int64_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  };
+  // Walk the group's SUPER-RUNS: a run of L pairs with one query track, extended by the following
+  // runs of L pairs whose reference tracks are the same, in the same order (the next queries of a
+  // reference band). A super-run of R queries packs its R queries' blocks into the rows and its L
+  // references' blocks into the columns: (query k, reference t) is pair s + k L + t. Its tiles
+  // are ceil(sum M / 32) x ceil(sum N / TW); u counts the super-runs' tiles in order (at most the
+  // per-pair tile count, so the grid's wt * ct slots per group hold them).
+  int s0 = 0, L = 0, R = 0, sumM = 0, sumN = 0, tb = 0, nct = 1;
   bool found = false;
-  while (rs < npp) {
-    const int a = __builtin_amdgcn_readlane(ga, rs);
-    re = rs;
-    cols = 0;
-    while (re < npp && __builtin_amdgcn_readlane(ga, re) == a) cols += __builtin_amdgcn_readlane(gn, re), ++re;
-    const int nt = (cols + TW - 1) / TW;
-    if (tc < tbase + nt) {
+  while (s0 < npp) {
+    const int a = __builtin_amdgcn_readlane(ga, s0);
+    int e = s0 + 1;
+    while (e < npp && __builtin_amdgcn_readlane(ga, e) == a) ++e;
+    L = e - s0;
+    sumN = 0;
+    for (int t = s0; t < e; ++t) sumN += __builtin_amdgcn_readlane(gn, t);
+    sumM = __builtin_amdgcn_readlane(gm, s0);
+    R = 1;
+    int f = e;
+    while (f + L <= npp) {  // absorb the next run if it is L pairs with the same references
+      const int a2 = __builtin_amdgcn_readlane(ga, f);
+      bool same = f + L == npp || __builtin_amdgcn_readlane(ga, f + L) != a2;
+      for (int t = 0; t < L && same; ++t)
+        same = __builtin_amdgcn_readlane(ga, f + t) == a2 &&
+               __builtin_amdgcn_readlane(gb, f + t) == __builtin_amdgcn_readlane(gb, s0 + t);
+      if (!same) break;
+      sumM += __builtin_amdgcn_readlane(gm, f);
+      ++R;
+      f += L;
+    }
+    nct = (sumN + TW - 1) / TW;
+    const int nt = (sumM + 31) / 32 * nct;
+    if (u < tb + nt) {
       found = true;
       break;
     }
-    tbase += nt;
-    rs = re;
+    tb += nt;
+    s0 = f;
   }
   if (!found) return;
-  const int M = __builtin_amdgcn_readlane(gm, rs);
-  const int64_t offa = ((int64_t)__builtin_amdgcn_readlane((int)(goa >> 32), rs) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)goa, rs);
-  const int bi = ti * 32;
-  if (bi >= M) return;
-  // this lane's packed columns (one per accumulator): pair q of the run, block c of its reference
+  const int rt = (u - tb) / nct, tc = (u - tb) - rt * nct;
+  // packed row gr -> (query k of the super-run, block within it); rows past sum M clamp to the last.
+  // Every lane runs every iteration and selects (no per-lane exit from a loop over readlane
+  // values: a value a lane keeps from an earlier iteration than its neighbours is divergent,
+  // which the compiler must not mistake for the uniform loop counter)
+  auto locate_row = [&](int gr, int* k, int* row, int64_t* offa) {
+    int pre = 0, kk_ = R - 1, row_ = 0;
+    int64_t off_ = 0;
+    bool done = false;
+    for (int kk = 0; kk < R; ++kk) {
+      const int m = __builtin_amdgcn_readlane(gm, s0 + kk * L);
+      const int64_t o = rl64(goa, s0 + kk * L);
+      const bool hit = !done && (gr < pre + m || kk == R - 1);
+      kk_ = hit ? kk : kk_;
+      row_ = hit ? min(gr - pre, m - 1) : row_;
+      off_ = hit ? o : off_;
+      done = done || hit;
+      pre += m;
+    }
+    *k = kk_;
+    *row = row_;
+    *offa = off_;
+  };
   const float* rows[NO];
-  rows[0] = bank + (offa + min(bi + r, M - 1)) * (int64_t)d + (KB / 2) * h;
-  int cq[NB], cc[NB];
+  {
+    int k, row;
+    int64_t offa;
+    locate_row(rt * 32 + r, &k, &row, &offa);
+    rows[0] = bank + (offa + row) * (int64_t)d + (KB / 2) * h;
+  }
+  // this lane's packed columns (one per accumulator): reference t of the super-run, block c
+  int ct_[NB], cc[NB];
   int64_t cob[NB];
   bool cvalid[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int gc = (tc - tbase) * TW + 32 * j + r;
-    cvalid[j] = gc < cols;
-    int q = re - 1, pre = 0, N = 1;
+    const int gc = tc * TW + 32 * j + r;
+    cvalid[j] = gc < sumN;
+    int t = L - 1, pre = 0, cpre = 0, N = 1;
     int64_t offb = 0;
-    for (int k = rs; k < re; ++k) {  // the last pair of the run takes every column past the others
-      const int n = __builtin_amdgcn_readlane(gn, k);
-      if (gc < pre + n || k == re - 1) {
-        q = k;
-        N = n;
-        offb = ((int64_t)__builtin_amdgcn_readlane((int)(gob >> 32), k) << 32) |
-               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gob, k);
-        break;
-      }
+    bool done = false;
+    for (int k = 0; k < L; ++k) {  // the last reference takes every column past the others
+      const int n = __builtin_amdgcn_readlane(gn, s0 + k);
+      const int64_t o = rl64(gob, s0 + k);
+      const bool hit = !done && (gc < pre + n || k == L - 1);
+      t = hit ? k : t;
+      N = hit ? n : N;
+      cpre = hit ? pre : cpre;
+      offb = hit ? o : offb;
+      done = done || hit;
       pre += n;
     }
-    cq[j] = q;
-    cc[j] = min(gc - pre, N - 1);  // clamped for the padding lanes (never stored)
+    ct_[j] = t;
+    cc[j] = min(gc - cpre, N - 1);  // clamped for the padding lanes (never stored)
     cob[j] = offb;
     rows[1 + j] = bank + (offb + cc[j]) * (int64_t)d + (KB / 2) * h;
   }
@@ -649,19 +698,23 @@ __global__ __launch_bounds__(256, ACOSS_EF_WPE) void k_ef_csm_pack(const float* 
                                                          : f32x4e{0.0f, 0.0f, 0.0f, 0.0f};
     mul(ring[0]);
   }
+  float sqc[NB];
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    if (!cvalid[j]) continue;
-    float* ob = out + (size_t)(p0 + cq[j]) * ld * ld + cc[j];
-    const float sqc = sq[cob[j] + cc[j]];
+  for (int j = 0; j < NB; ++j) sqc[j] = sq[cob[j] + cc[j]];
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int row = bi + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      if (row < M) {
-        float c2 = (sq[offa + row] + sqc) - 2.0f * acc[j][reg];
-        if (c2 < 0.0f) c2 = 0.0f;
-        ob[(size_t)row * ld] = sqrtf(c2);
-      }
+  for (int reg = 0; reg < 16; ++reg) {
+    const int gr = rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    if (gr >= sumM) continue;
+    int k, row;
+    int64_t offa;
+    locate_row(gr, &k, &row, &offa);
+    const float sqr = sq[offa + row];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (!cvalid[j]) continue;
+      float c2 = (sqr + sqc[j]) - 2.0f * acc[j][reg];
+      if (c2 < 0.0f) c2 = 0.0f;
+      out[(size_t)(p0 + s0 + k * L + ct_[j]) * ld * ld + (size_t)row * ld + cc[j]] = sqrtf(c2);
     }
   }
 }
@@ -1185,6 +1238,9 @@ extern "C" int acoss_earlyfusion(const float* mfcc, const float* ssm, const floa
   int64_t chunk = (int64_t)(budget / nset / per_pair);
   if (chunk < 1) chunk = 1;
   if (chunk > 65535) chunk = 65535;
+  // sub-batches start at multiples of the packing group (k_ef_csm_pack), so the caller's runs of
+  // one query stay aligned with the groups
+  if (chunk > kEfPack) chunk -= chunk % kEfPack;
   if (chunk > n_pairs) chunk = n_pairs;
   char* ws = static_cast<char*>(workspace(11, nset * (per_pair * chunk + 16 * 256)));
   if (!ws) return ACOSS_E_HIP;
