@@ -1139,9 +1139,9 @@ __global__ void k_ef_wsum(float* __restrict__ C, int64_t mat_stride, int ld, EfP
   const int p = blockIdx.y;
   int a, b, M, N;
   pair_dims(E, p, &a, &b, &M, &N);
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (int64_t)M * N) return;
-  const int i = (int)(e / N), j = (int)(e - (int64_t)i * N);
+  const unsigned e = blockIdx.x * blockDim.x + threadIdx.x;  // M N <= ld^2 < 2^31: 32-bit division
+  if (e >= (unsigned)(M * N)) return;
+  const int i = (int)(e / (unsigned)N), j = (int)(e - (unsigned)i * (unsigned)N);
   const size_t idx = (size_t)p * ld * ld + (size_t)i * ld + j;
   float wsum = 0.0f;
 #pragma unroll
