@@ -475,6 +475,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 // gives the row's minimum, merged into the pair's row-minimum keys by one global atomic per step.
 // What this removes from the VALU: the 12 fma of every dot and the per-step frame hand-over (the
 // K = 4 kernel's 26 DPP moves), about half of its instructions per cell.
+#ifndef ACOSS_SIMPLE_PF
+#define ACOSS_SIMPLE_PF 1
+#endif
 constexpr int kKM = 2;                   // diagonals per lane
 constexpr int kDW = 64 * kKM;            // diagonals per wave
 constexpr int kGT = kDW / 16 + 1;        // 16 x 16 tiles per 16-step block
@@ -560,6 +563,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     load_a(x_lo);
 #pragma unroll
     for (int tt = 0; tt < kGT; ++tt) load_b(x_lo, tt);
+#if ACOSS_SIMPLE_PF
+    // the window norms a block needs (17 reference columns per lane, one query row per lane 0..15)
+    // are loaded one block ahead, raw (clamped index, masked where used): the first step no longer
+    // waits out a global load every block
+    double sbn[16 + kKM - 1], san;
+    auto load_norms = [&](int xb) {
+#pragma unroll
+      for (int q = 0; q < 16 + kKM - 1; ++q) sbn[q] = Wb[min(max(xb - (L - 1) + yl + q, 0), Q - 1)];
+      san = Wa[min(max(xb + (lane & 15) - (L - 1), 0), P - 1)];
+    };
+    load_norms(x_lo);
+#endif
     for (int x0 = x_lo; x0 <= x_hi; x0 += 16) {
       // ---- produce: G(x0 + s, x0 + ob + d) for s < 16, d < kDW into LDS [s][d]: the MFMAs, then
       // branch-free stores (a dot outside the wave's diagonals goes to the row's pad slot kDW,
@@ -592,6 +607,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       // MFMA operands (in flight during the 16 steps)
       const int i0 = x0 - (L - 1) + yl;
       double sbv[16 + kKM - 1];
+#if ACOSS_SIMPLE_PF
+#pragma unroll
+      for (int q = 0; q < 16 + kKM - 1; ++q) sbv[q] = (i0 + q >= 0 && i0 + q < Q) ? sbn[q] : kInf;
+      const double sa_l = san;
+      load_ops(x0 + 16);
+      load_norms(x0 + 16);
+#else
 #pragma unroll
       for (int q = 0; q < 16 + kKM - 1; ++q) {  // clamped loads, then a select: no branch per load
         const int cc = i0 + q;
@@ -599,6 +621,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         sbv[q] = (cc >= 0 && cc < Q) ? v : kInf;
       }
       load_ops(x0 + 16);
+#endif
       // the block's dots of this lane's diagonals, all 16 steps read at once (no LDS latency inside
       // the steps), and the 16 query window norms (lane s: row x0 + s - 9; read per step by readlane,
       // so no scalar load shares lgkmcnt with the LDS reads inside the steps)
@@ -607,7 +630,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       for (int s = 0; s < 16; ++s)
 #pragma unroll
         for (int k = 0; k < kKM; ++k) gall[s][k] = G[s * kGS + kKM * lane + k];
+#if !ACOSS_SIMPLE_PF
       const double sa_l = Wa[min(max(x0 + (lane & 15) - (L - 1), 0), P - 1)];
+#endif
       // per step: the lane minimum over its diagonals; after the 16 steps the minima go over the G
       // rows (every read is done) and four lanes per row fold the row's 64 lane minima (16 each,
       // then a quad minimum) -- instead of one dependent 6-stage DPP wave minimum per step
