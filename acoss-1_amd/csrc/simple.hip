@@ -469,15 +469,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 // computed as DW / 16 + 1 tiles of 16 x 16 by three chained MFMAs each (K = 12 bins in chunks of 4:
 // measured equal to the sequential fma chain, profiles/r05/mfma_probe; the chain starts from -0,
 // so a zero first product keeps its sign exactly as the canonical first product does) and staged
-// in LDS by (step, diagonal); then each step reads its lane's KM dots (one ds_read2_b64), adds them
-// into the open windows (a shift register per diagonal: W[a] = the a most recent dots, so the
-// completed window W[9] + g is the sequential sum in canonical order), and one DPP wave minimum
-// gives the row's minimum, merged into the pair's row-minimum keys by one global atomic per step.
+// in LDS by (step, diagonal); then each step adds its lane's KM dots into the open windows (a shift
+// register per diagonal: W[a] = the a most recent dots, so the completed window W[9] + g is the
+// sequential sum in canonical order). The MFMA tiles of block b + 1 are issued between block b's
+// steps (G is free once those steps' dots are read), and the 16 steps' lane minima are reduced
+// over the wave in registers (permlane32 / permlane16 swaps, then DPP: each 4-lane quad ends with
+// one step's row minimum) and merged into the pair's row-minimum keys by one global atomic per row.
 // What this removes from the VALU: the 12 fma of every dot and the per-step frame hand-over (the
-// K = 4 kernel's 26 DPP moves), about half of its instructions per cell.
-#ifndef ACOSS_SIMPLE_PF
-#define ACOSS_SIMPLE_PF 1
-#endif
+// K = 4 kernel's 26 DPP moves), about half of its instructions per cell. Measured steps:
+// profiles/r06/simple_mfma/README.txt.
+
+// f64 lane exchanges for the step-minimum reduce-scatter of k_simple_mfma (two 32-bit halves each)
+__device__ __forceinline__ void swap32_f64(double& x, double& y) {  // x' = [x_lo, y_lo], y' = [x_hi, y_hi]
+  const unsigned long long ux = __builtin_bit_cast(unsigned long long, x), uy = __builtin_bit_cast(unsigned long long, y);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ux, (unsigned)uy, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ux >> 32), (unsigned)(uy >> 32), false, false);
+  x = __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi[0] << 32) | (unsigned)lo[0]);
+  y = __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi[1] << 32) | (unsigned)lo[1]);
+}
+__device__ __forceinline__ void swap16_f64(double& x, double& y) {  // x' = rows [x0 y0 x2 y2], y' = [x1 y1 x3 y3]
+  const unsigned long long ux = __builtin_bit_cast(unsigned long long, x), uy = __builtin_bit_cast(unsigned long long, y);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ux, (unsigned)uy, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ux >> 32), (unsigned)(uy >> 32), false, false);
+  x = __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi[0] << 32) | (unsigned)lo[0]);
+  y = __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi[1] << 32) | (unsigned)lo[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {  // every lane reads its DPP source (full masks)
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = dpp_u32<CTRL>(0u, (unsigned)u), hi = dpp_u32<CTRL>(0u, (unsigned)(u >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+// Pair (x, y) across lanes l and l ^ D (D = 8 or 4, within 16-lane rows): lanes with bit D clear keep
+// min(x, x from l ^ D), the others min(y, y from l ^ D).
+template <int D>
+__device__ __forceinline__ double xpair_min(double x, double y, int lane) {
+  const bool hi = (lane & D) != 0;
+  const double send = hi ? x : y, keep = hi ? y : x;
+  double recv;
+  if constexpr (D == 8) {
+    recv = dpp_f64<0x128>(send);  // row_ror:8 = lane ^ 8 within the row
+  } else {
+    const double from_up = dpp_f64<0x12C>(send);   // row_ror:12: lane l reads l + 4
+    const double from_down = dpp_f64<0x124>(send); // row_ror:4: lane l reads l - 4
+    recv = hi ? from_down : from_up;
+  }
+  return vmin_f64(keep, recv);
+}
 constexpr int kKM = 2;                   // diagonals per lane
 constexpr int kDW = 64 * kKM;            // diagonals per wave
 constexpr int kGT = kDW / 16 + 1;        // 16 x 16 tiles per 16-step block
@@ -552,129 +590,132 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       bv[tt][1] = br[4];
       bv[tt][2] = br[8];
     };
-    auto load_ops = [&](int xb) {  // the next block's operands (after the current block's MFMAs)
-      load_a(xb);
-#pragma unroll
-      for (int tt = 0; tt < kGT - 1; ++tt)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) bv[tt][c] = bv[tt + 1][c];
-      load_b(xb, kGT - 1);
-    };
     load_a(x_lo);
 #pragma unroll
     for (int tt = 0; tt < kGT; ++tt) load_b(x_lo, tt);
-#if ACOSS_SIMPLE_PF
-    // the window norms a block needs (17 reference columns per lane, one query row per lane 0..15)
-    // are loaded one block ahead, raw (clamped index, masked where used): the first step no longer
-    // waits out a global load every block
-    double sbn[16 + kKM - 1], san;
-    auto load_norms = [&](int xb) {
+    // Producer / consumer overlapped: block b's steps issue block b + 1's MFMA tiles (tile t at step
+    // kP0 + t, its four results stored to G one step later; G is free once the steps' dots are
+    // read), and the step minima are reduced in registers (a permlane32 / permlane16 /
+    // DPP reduce-scatter folded into the steps), so G holds nothing else. Operands: a / bv hold
+    // block b + 1's (a from an, loaded a block ahead); after tile 8 the B tiles shift down one
+    // and the last tile of block b + 2 is loaded.
+    auto store_tile = [&](const f64x4m& acc, int tt) {
 #pragma unroll
-      for (int q = 0; q < 16 + kKM - 1; ++q) sbn[q] = Wb[min(max(xb - (L - 1) + yl + q, 0), Q - 1)];
-      san = Wa[min(max(xb + (lane & 15) - (L - 1), 0), P - 1)];
+      for (int r = 0; r < 4; ++r) {
+        const int s = lk + 4 * r;
+        const int d = 16 * tt + li - s;
+        if (tt == 0 || tt == kGT - 1)
+          G[s * kGS + ((d >= 0 && d < kDW) ? d : kDW)] = acc[r];
+        else
+          G[(kGS - 1) * s + li + 16 * tt] = acc[r];
+      }
     };
-    load_norms(x_lo);
-#endif
+    // block 0's dots, then block 1's operands
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // the previous group's reads of G are done
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int tt = 0; tt < kGT; ++tt) {
+      f64x4m acc = {-0.0, -0.0, -0.0, -0.0};
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bv[tt][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bv[tt][1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, bv[tt][2], acc, 0, 0, 0);
+      store_tile(acc, tt);
+    }
+    load_a(x_lo + 16);
+#pragma unroll
+    for (int tt = 0; tt < kGT - 1; ++tt)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) bv[tt][c] = bv[tt + 1][c];
+    load_b(x_lo + 16, kGT - 1);
+    // the block's reference window norms, raw (clamped column; masked where used). Register q is
+    // reloaded with the next block's column once step q has used it (16 steps ahead of its use)
+    double sbv[16 + kKM - 1];
+#pragma unroll
+    for (int q = 0; q < 16 + kKM - 1; ++q) sbv[q] = Wb[min(max(x_lo - (L - 1) + yl + q, 0), Q - 1)];
+    double san = Wa[min(max(x_lo + (lane & 15) - (L - 1), 0), P - 1)];
     for (int x0 = x_lo; x0 <= x_hi; x0 += 16) {
-      // ---- produce: G(x0 + s, x0 + ob + d) for s < 16, d < kDW into LDS [s][d]: the MFMAs, then
-      // branch-free stores (a dot outside the wave's diagonals goes to the row's pad slot kDW,
-      // which no step reads)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();  // the previous block's reads of G are done
+      __builtin_amdgcn_wave_barrier();  // this block's dots are in G
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (int tt = 0; tt < kGT; ++tt) {
-        f64x4m acc = {-0.0, -0.0, -0.0, -0.0};
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bv[tt][0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bv[tt][1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, bv[tt][2], acc, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int s = lk + 4 * r;
-          const int d = 16 * tt + li - s;  // in [16 tt - 15, 16 tt + 15]: only the end tiles can leave [0, kDW)
-          if (tt == 0 || tt == kGT - 1)
-            G[s * kGS + ((d >= 0 && d < kDW) ? d : kDW)] = acc[r];
-          else
-            G[(kGS - 1) * s + li + 16 * tt] = acc[r];
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // ---- consume: 16 steps of windows + row minima, unrolled (static step index) ----
       const int send = min(16, x_hi - x0 + 1);
-      // the block's reference window norms (columns x0 - 9 + yl + 0..16), then the next block's
-      // MFMA operands (in flight during the 16 steps)
       const int i0 = x0 - (L - 1) + yl;
-      double sbv[16 + kKM - 1];
-#if ACOSS_SIMPLE_PF
-#pragma unroll
-      for (int q = 0; q < 16 + kKM - 1; ++q) sbv[q] = (i0 + q >= 0 && i0 + q < Q) ? sbn[q] : kInf;
       const double sa_l = san;
-      load_ops(x0 + 16);
-      load_norms(x0 + 16);
-#else
-#pragma unroll
-      for (int q = 0; q < 16 + kKM - 1; ++q) {  // clamped loads, then a select: no branch per load
-        const int cc = i0 + q;
-        const double v = Wb[min(max(cc, 0), Q - 1)];
-        sbv[q] = (cc >= 0 && cc < Q) ? v : kInf;
-      }
-      load_ops(x0 + 16);
-#endif
-      // the block's dots of this lane's diagonals, all 16 steps read at once (no LDS latency inside
-      // the steps), and the 16 query window norms (lane s: row x0 + s - 9; read per step by readlane,
-      // so no scalar load shares lgkmcnt with the LDS reads inside the steps)
+      san = Wa[min(max(x0 + 16 + (lane & 15) - (L - 1), 0), P - 1)];
+      // the dots of steps 0..7 now, of steps 8..15 at step kP0 (before the first store into G:
+      // LDS ops of one wave run in order), so only half of them are live through the first steps
+      constexpr int kP0 = 16 - kGT - 1;  // step of block b + 1's tile 0 (its last tile stored at step 15)
       double gall[16][kKM];
 #pragma unroll
-      for (int s = 0; s < 16; ++s)
+      for (int s = 0; s < 8; ++s)
 #pragma unroll
         for (int k = 0; k < kKM; ++k) gall[s][k] = G[s * kGS + kKM * lane + k];
-#if !ACOSS_SIMPLE_PF
-      const double sa_l = Wa[min(max(x0 + (lane & 15) - (L - 1), 0), P - 1)];
-#endif
-      // per step: the lane minimum over its diagonals; after the 16 steps the minima go over the G
-      // rows (every read is done) and four lanes per row fold the row's 64 lane minima (16 each,
-      // then a quad minimum) -- instead of one dependent 6-stage DPP wave minimum per step
-      // every step runs (no branch between steps, so the scheduler can overlap them): the steps of
-      // a last block past x_hi read clamped rows, and their minima are dropped below. A step's lane
-      // minimum goes straight over its G row (every read of the block is done: LDS ops of one wave
-      // run in order)
+      f64x4m acc[kGT];
+      double mv[16], ra[8], rb[4], rc[2];
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        {
-          const double sar = __builtin_bit_cast(double,
-              ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(__builtin_bit_cast(unsigned long long, sa_l) >> 32), s) << 32) |
-              (unsigned)__builtin_amdgcn_readlane((int)(unsigned)__builtin_bit_cast(unsigned long long, sa_l), s));
-          double m = kInf;
+        if (s == kP0) {
 #pragma unroll
-          for (int k = 0; k < kKM; ++k) {
-            const double qt = W[k][L - 1] + gall[s][k];
-            m = vmin_f64(m, fma(-2.0, qt, sbv[s + k] + sar));
-          }
+          for (int s2 = 8; s2 < 16; ++s2)
 #pragma unroll
-          for (int k = 0; k < kKM; ++k) {
-#pragma unroll
-            for (int a = L - 1; a >= 2; --a) W[k][a] = W[k][a - 1] + gall[s][k];
-            W[k][1] = gall[s][k];
-          }
-          G[s * kGS + lane] = m;
+            for (int k = 0; k < kKM; ++k) gall[s2][k] = G[s2 * kGS + kKM * lane + k];
         }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      {
-        const int row = lane >> 2, seg = lane & 3;
-        const double* src = G + row * kGS + 16 * seg;
-        double v = src[0];
+        const int tt = s - kP0;  // block b + 1's tile tt at step kP0 + tt
+        if (tt >= 0 && tt < kGT) {
+          acc[tt] = f64x4m{-0.0, -0.0, -0.0, -0.0};
+          acc[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bv[tt][0], acc[tt], 0, 0, 0);
+          acc[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bv[tt][1], acc[tt], 0, 0, 0);
+          acc[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, bv[tt][2], acc[tt], 0, 0, 0);
+        }
+        if (tt == kGT - 1) {  // every tile issued: block b + 2's operands (B shifted, fresh A and last tile)
+          load_a(x0 + 32);
 #pragma unroll
-        for (int i = 1; i < 16; ++i) v = vmin_f64(v, src[i]);
-        v = vmin_f64(v, __shfl_xor(v, 1));
-        v = vmin_f64(v, __shfl_xor(v, 2));
-        const int r = x0 + row - (L - 1);
-        if (seg == 0 && row < send && r >= 0 && r < P && v < kInf) atomicMin(&mpk[r], dkey(v));
+          for (int tt = 0; tt < kGT - 1; ++tt)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) bv[tt][c] = bv[tt + 1][c];
+          load_b(x0 + 32, kGT - 1);
+        }
+        const double sar = __builtin_bit_cast(double,
+            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(__builtin_bit_cast(unsigned long long, sa_l) >> 32), s) << 32) |
+            (unsigned)__builtin_amdgcn_readlane((int)(unsigned)__builtin_bit_cast(unsigned long long, sa_l), s));
+        double m = kInf;
+#pragma unroll
+        for (int k = 0; k < kKM; ++k) {
+          const double qt = W[k][L - 1] + gall[s][k];
+          const double sb = (i0 + s + k >= 0 && i0 + s + k < Q) ? sbv[s + k] : kInf;
+          m = vmin_f64(m, fma(-2.0, qt, sb + sar));
+        }
+#pragma unroll
+        for (int k = 0; k < kKM; ++k) {
+#pragma unroll
+          for (int a = L - 1; a >= 2; --a) W[k][a] = W[k][a - 1] + gall[s][k];
+          W[k][1] = gall[s][k];
+        }
+        sbv[s] = Wb[min(max(i0 + 16 + s, 0), Q - 1)];  // the next block's column s
+        if (s == 15) sbv[16] = Wb[min(max(i0 + 32, 0), Q - 1)];
+        // reduce-scatter of the 16 step minima over the 64 lanes, as the steps complete
+        mv[s] = m;
+        if (s & 1) {  // lanes l, l ^ 32: lanes < 32 keep step s - 1, the others step s
+          double x = mv[s - 1], y = mv[s];
+          swap32_f64(x, y);
+          ra[s >> 1] = vmin_f64(x, y);
+        }
+        if ((s & 3) == 3) {  // lanes l, l ^ 16
+          double x = ra[(s >> 1) - 1], y = ra[s >> 1];
+          swap16_f64(x, y);
+          rb[s >> 2] = vmin_f64(x, y);
+        }
+        if ((s & 7) == 7) rc[s >> 3] = xpair_min<8>(rb[(s >> 2) - 1], rb[s >> 2], lane);  // lanes l, l ^ 8
+        if (tt >= 1 && tt <= kGT) store_tile(acc[tt - 1], tt - 1);  // a step after its MFMAs (their latency)
+        __builtin_amdgcn_sched_barrier(0);    // one step per scheduling region: no tile's MFMAs hoisted
       }
+      double v = xpair_min<4>(rc[0], rc[1], lane);  // lanes l, l ^ 4
+      v = vmin_f64(v, dpp_f64<0x4E>(v));               // quad_perm [2,3,0,1]: l ^ 2
+      v = vmin_f64(v, dpp_f64<0xB1>(v));               // quad_perm [1,0,3,2]: l ^ 1
+      // lane l now holds the minimum of step 8 b2 + 4 b3 + 2 b4 + b5 (bi = bit i of l)
+      const int step = 8 * ((lane >> 2) & 1) + 4 * ((lane >> 3) & 1) + 2 * ((lane >> 4) & 1) + ((lane >> 5) & 1);
+      const int r = x0 + step - (L - 1);
+      if ((lane & 3) == 0 && step < send && r >= 0 && r < P && v < kInf) atomicMin(&mpk[r], dkey(v));
     }
   }
   __threadfence();
