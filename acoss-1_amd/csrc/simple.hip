@@ -77,31 +77,59 @@ __global__ void k_simple_mark(const int32_t* __restrict__ pairs, int64_t n_pairs
   }
 }
 
+// The MFMA kernel reads the window norms from a padded copy (k_simple_track's wpad): every flagged
+// track's norms at woff[t] = toff[t] + kWPad (rank + 1), with kWPad +inf entries before the first
+// track and after every track, so its reads past either end of a track need neither a clamped index
+// nor a mask (they fall in [-136, Q + 157] around the track; an out-of-range column's +inf is
+// exactly the masked value).
+constexpr int kWPad = 256;
+
 __global__ __launch_bounds__(1024) void k_simple_scan(const int32_t* __restrict__ len, const int32_t* __restrict__ used,
                                                       int n_tracks, int64_t* __restrict__ toff,
-                                                      int64_t* __restrict__ total) {
-  __shared__ int64_t wsum[16];
+                                                      int64_t* __restrict__ woff, int64_t* __restrict__ total) {
+  __shared__ int64_t wsum[16], wcnt[16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int per = (n_tracks + 1023) / 1024;
   const int a = min(n_tracks, t * per), b = min(n_tracks, a + per);
-  int64_t mine = 0;
-  for (int u = a; u < b; ++u) mine += used[u] ? (int64_t)align_up((size_t)len[u], 8) : 0;
-  // inclusive scan of the per-thread sums: within the wave, then across the 16 waves
-  int64_t x = mine;
-  for (int d = 1; d < 64; d <<= 1) {
-    const int64_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
+  int64_t mine = 0, mcnt = 0;
+  for (int u = a; u < b; ++u) {
+    mine += used[u] ? (int64_t)align_up((size_t)len[u], 8) : 0;
+    mcnt += used[u] ? 1 : 0;
   }
-  if (lane == 63) wsum[w] = x;
+  // inclusive scans of the per-thread sums: within the wave, then across the 16 waves
+  int64_t x = mine, c = mcnt;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(x, d, 64), z = __shfl_up(c, d, 64);
+    if (lane >= d) {
+      x += y;
+      c += z;
+    }
+  }
+  if (lane == 63) {
+    wsum[w] = x;
+    wcnt[w] = c;
+  }
   __syncthreads();
-  int64_t before = 0;
-  for (int v = 0; v < w; ++v) before += wsum[v];
-  int64_t run = before + x - mine;  // exclusive prefix of this thread
+  int64_t before = 0, cbefore = 0;
+  for (int v = 0; v < w; ++v) {
+    before += wsum[v];
+    cbefore += wcnt[v];
+  }
+  int64_t run = before + x - mine, rank = cbefore + c - mcnt;  // exclusive prefixes of this thread
   for (int u = a; u < b; ++u) {
     toff[u] = used[u] ? run : -1;
+    woff[u] = used[u] ? run + kWPad * (rank + 1) : -1;
     run += used[u] ? (int64_t)align_up((size_t)len[u], 8) : 0;
+    rank += used[u] ? 1 : 0;
   }
-  if (t == 1023) *total = run;
+  if (t == 1023) {
+    total[0] = run;
+    total[1] = rank;
+  }
+}
+
+__global__ void k_fill_f64(double* __restrict__ x, int64_t n, double v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) x[i] = v;
 }
 
 // per flagged track: chroma profile (sum over time, sequential), per-frame squared norms (fma
@@ -110,7 +138,8 @@ __global__ __launch_bounds__(1024) void k_simple_scan(const int32_t* __restrict_
 __global__ void k_simple_track(const double* __restrict__ feats, const int64_t* __restrict__ off,
                                const int32_t* __restrict__ len, int n_tracks, int L, double* __restrict__ prof,
                                double* __restrict__ fnorm, double* __restrict__ wnorm, double* __restrict__ ext,
-                               double* __restrict__ rec, const int64_t* __restrict__ toff, int copies) {
+                               double* __restrict__ rec, const int64_t* __restrict__ toff, int copies,
+                               double* __restrict__ wpad, const int64_t* __restrict__ woff) {
   const int tr = blockIdx.x;
   if (tr >= n_tracks || toff[tr] < 0) return;
   const double* S = feats + off[tr];
@@ -144,6 +173,7 @@ __global__ void k_simple_track(const double* __restrict__ feats, const int64_t* 
     double acc = 0.0;
     for (int u = 0; u < L; ++u) acc = acc + fnorm[o + i + u];
     wnorm[o + i] = acc;
+    if (wpad) wpad[woff[tr] + i] = acc;
   }
 }
 
@@ -524,9 +554,9 @@ typedef double f64x4m __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_simple_mfma(
     const double* __restrict__ ext, const double* __restrict__ rec, const int32_t* __restrict__ len,
-    const int32_t* __restrict__ pairs, const double* __restrict__ prof, const double* __restrict__ wnorm,
-    const int64_t* __restrict__ toff, int n2max, int64_t n_pairs, int apply_oti, unsigned long long* __restrict__ mpk_g,
-    double* __restrict__ score, int32_t* __restrict__ oti_out) {
+    const int32_t* __restrict__ pairs, const double* __restrict__ prof, const double* __restrict__ wpad,
+    const int64_t* __restrict__ woff, const int64_t* __restrict__ toff, int n2max, int64_t n_pairs, int apply_oti,
+    unsigned long long* __restrict__ mpk_g, double* __restrict__ score, int32_t* __restrict__ oti_out) {
   constexpr int L = kFastL;
   extern __shared__ double gsm[];  // 4 waves x 16 x kGS doubles; reused for the final sort
   __shared__ int s_k;
@@ -553,8 +583,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int64_t oa = toff[ta], ob0 = toff[tb];
   const double* Ea = ext + (size_t)oa * kExt + kq;  // query bin (j + kq) mod 12 at offset j
   const double* Rb = rec + (size_t)ob0 * kRec;
-  const double* Wa = wnorm + oa;
-  const double* Wb = wnorm + ob0;
+  const double* Wa = wpad + woff[ta];  // padded with +inf on both sides (kWPad)
+  const double* Wb = wpad + woff[tb];
   double* G = gsm + (size_t)wave * 16 * kGS;
   const int ND = P + Q - 1;
   const int NG = (ND + kDW - 1) / kDW;
@@ -628,12 +658,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
       for (int c = 0; c < 3; ++c) bv[tt][c] = bv[tt + 1][c];
     load_b(x_lo + 16, kGT - 1);
-    // the block's reference window norms, raw (clamped column; masked where used). Register q is
-    // reloaded with the next block's column once step q has used it (16 steps ahead of its use)
+    // the block's reference window norms (+inf past the track's ends, from the padded copy). Register
+    // q is reloaded with the next block's column once step q has used it (16 steps ahead of its use)
     double sbv[16 + kKM - 1];
 #pragma unroll
-    for (int q = 0; q < 16 + kKM - 1; ++q) sbv[q] = Wb[min(max(x_lo - (L - 1) + yl + q, 0), Q - 1)];
-    double san = Wa[min(max(x_lo + (lane & 15) - (L - 1), 0), P - 1)];
+    for (int q = 0; q < 16 + kKM - 1; ++q) sbv[q] = Wb[x_lo - (L - 1) + yl + q];
+    double san = Wa[x_lo + (lane & 15) - (L - 1)];
     for (int x0 = x_lo; x0 <= x_hi; x0 += 16) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();  // this block's dots are in G
@@ -641,7 +671,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       const int send = min(16, x_hi - x0 + 1);
       const int i0 = x0 - (L - 1) + yl;
       const double sa_l = san;
-      san = Wa[min(max(x0 + 16 + (lane & 15) - (L - 1), 0), P - 1)];
+      san = Wa[x0 + 16 + (lane & 15) - (L - 1)];
       // the dots of steps 0..7 now, of steps 8..15 at step kP0 (before the first store into G:
       // LDS ops of one wave run in order), so only half of them are live through the first steps
       constexpr int kP0 = 16 - kGT - 1;  // step of block b + 1's tile 0 (its last tile stored at step 15)
@@ -682,8 +712,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
         for (int k = 0; k < kKM; ++k) {
           const double qt = W[k][L - 1] + gall[s][k];
-          const double sb = (i0 + s + k >= 0 && i0 + s + k < Q) ? sbv[s + k] : kInf;
-          m = vmin_f64(m, fma(-2.0, qt, sb + sar));
+          m = vmin_f64(m, fma(-2.0, qt, sbv[s + k] + sar));
         }
 #pragma unroll
         for (int k = 0; k < kKM; ++k) {
@@ -691,8 +720,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
           for (int a = L - 1; a >= 2; --a) W[k][a] = W[k][a - 1] + gall[s][k];
           W[k][1] = gall[s][k];
         }
-        sbv[s] = Wb[min(max(i0 + 16 + s, 0), Q - 1)];  // the next block's column s
-        if (s == 15) sbv[16] = Wb[min(max(i0 + 32, 0), Q - 1)];
+        sbv[s] = Wb[i0 + 16 + s];  // the next block's column s
+        if (s == 15) sbv[16] = Wb[i0 + 32];
         // reduce-scatter of the 16 step minima over the 64 lanes, as the steps complete
         mv[s] = m;
         if (s & 1) {  // lanes l, l ^ 32: lanes < 32 keep step s - 1, the others step s
@@ -792,31 +821,46 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
   const size_t prof_bytes = align_up((size_t)n_tracks * 12 * 8, 256);
   const size_t toff_bytes = align_up((size_t)n_tracks * 8, 256);
   const size_t used_bytes = align_up((size_t)n_tracks * 4, 256);
-  const size_t head = prof_bytes + toff_bytes + used_bytes + 256;
+  // the MFMA kernel (frame dots on v_mfma_f64_16x16x4_f64), bit-identical to the VALU kernels: the
+  // default for tracks of >= 256 frames (the VALU kernels pack several short pairs per block:
+  // 200 frames 6.8M vs 5.5M pairs/s; profiles/r06/simple_mfma/); ACOSS_SIMPLE_MFMA=0 / 1 forces either
+  const char* menv = getenv("ACOSS_SIMPLE_MFMA");
+  const bool mfma = fast && (menv ? menv[0] == '1' : max_len >= 256);
+  const size_t head = prof_bytes + 2 * toff_bytes + used_bytes + 256;
   char* hd = static_cast<char*>(workspace(8, head));
   if (!hd) return ACOSS_E_HIP;
   double* prof = reinterpret_cast<double*>(hd);
   int64_t* toff = reinterpret_cast<int64_t*>(hd + prof_bytes);
-  int32_t* used = reinterpret_cast<int32_t*>(hd + prof_bytes + toff_bytes);
-  int64_t* d_total = reinterpret_cast<int64_t*>(hd + prof_bytes + toff_bytes + used_bytes);
+  int64_t* woff = reinterpret_cast<int64_t*>(hd + prof_bytes + toff_bytes);
+  int32_t* used = reinterpret_cast<int32_t*>(hd + prof_bytes + 2 * toff_bytes);
+  int64_t* d_total = reinterpret_cast<int64_t*>(hd + prof_bytes + 2 * toff_bytes + used_bytes);
   ACOSS_HIP_CHECK(hipMemsetAsync(used, 0, used_bytes, s));
   hipLaunchKernelGGL(k_simple_mark, dim3((unsigned)((n_pairs + 255) / 256)), dim3(256), 0, s, pairs, n_pairs, used);
   ACOSS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_simple_scan, dim3(1), dim3(1024), 0, s, track_len, used, n_tracks, toff, d_total);
+  hipLaunchKernelGGL(k_simple_scan, dim3(1), dim3(1024), 0, s, track_len, used, n_tracks, toff, woff, d_total);
   ACOSS_LAUNCH_CHECK();
-  int64_t frames = 0;
-  ACOSS_HIP_CHECK(hipMemcpyAsync(&frames, d_total, 8, hipMemcpyDeviceToHost, s));
+  int64_t tot[2] = {0, 0};  // frames, flagged tracks
+  ACOSS_HIP_CHECK(hipMemcpyAsync(tot, d_total, 16, hipMemcpyDeviceToHost, s));
   ACOSS_HIP_CHECK(hipStreamSynchronize(s));
+  const int64_t frames = tot[0];
   const size_t vec_bytes = align_up((size_t)std::max<int64_t>(frames, 8) * 8, 256);
-  const size_t bytes = 2 * vec_bytes + (fast ? vec_bytes * (kExt + kRec) : 0);
+  const int64_t wpad_n = mfma ? frames + (int64_t)kWPad * (tot[1] + 1) : 0;
+  const size_t wpad_bytes = align_up((size_t)wpad_n * 8, 256);
+  const size_t bytes = 2 * vec_bytes + (fast ? vec_bytes * (kExt + kRec) : 0) + wpad_bytes;
   char* ws = static_cast<char*>(workspace(13, bytes));
   if (!ws) return ACOSS_E_HIP;
   double* fnorm = reinterpret_cast<double*>(ws);
   double* wnorm = reinterpret_cast<double*>(ws + vec_bytes);
   double* ext = reinterpret_cast<double*>(ws + 2 * vec_bytes);
   double* rec = reinterpret_cast<double*>(ws + 2 * vec_bytes + vec_bytes * kExt);
+  double* wpad = mfma ? reinterpret_cast<double*>(ws + 2 * vec_bytes + (fast ? vec_bytes * (kExt + kRec) : 0)) : nullptr;
+  if (mfma) {
+    hipLaunchKernelGGL(k_fill_f64, dim3((unsigned)std::min<int64_t>((wpad_n + 255) / 256, 4096)), dim3(256), 0, s, wpad,
+                       wpad_n, __builtin_inf());
+    ACOSS_LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(k_simple_track, dim3(n_tracks), dim3(256), 0, s, feats, track_off, track_len, n_tracks, sslen,
-                     prof, fnorm, wnorm, ext, rec, toff, fast ? 1 : 0);
+                     prof, fnorm, wnorm, ext, rec, toff, fast ? 1 : 0, wpad, woff);
   ACOSS_LAUNCH_CHECK();
   const int n2max = pow2_at_least(max(max_len - kFastL + 1, 2));
   const int sboff = n2max;
@@ -841,13 +885,6 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
   const int red = red_kernel ? (renv ? atoi(renv) : (ppb > 1 ? 1 : 0)) : 0;
   const int rboff = ppb * slotsz;
   const size_t lds = ((size_t)rboff + (red ? (size_t)4 * U * kRbufStride : 0)) * 8;
-  // the MFMA kernel (frame dots on v_mfma_f64_16x16x4_f64) with ACOSS_SIMPLE_MFMA=1: bit-identical,
-  // opt-in while it measures slower than the VALU kernels (profiles/r06/simple_mfma/)
-  // default for tracks of >= 256 frames (the VALU kernels pack several short pairs per block:
-  // 200 frames 6.9M vs 4.2M pairs/s; 500 frames 1.22x, 2,000 frames 1.10x for the MFMA kernel,
-  // profiles/r06/simple_mfma/); ACOSS_SIMPLE_MFMA=0 / 1 forces either
-  const char* menv = getenv("ACOSS_SIMPLE_MFMA");
-  const bool mfma = fast && (menv ? menv[0] == '1' : max_len >= 256);
   if (mfma) {
     // one block per pair; the pair's row-minimum keys in a global slot of its own (n2max keys),
     // so a launch takes at most 256 MB of them
@@ -861,7 +898,7 @@ extern "C" int acoss_simple_mp(const double* feats, const int64_t* track_off, co
     for (int64_t p0 = 0; p0 < n_pairs; p0 += per) {
       const int64_t np = std::min<int64_t>(n_pairs - p0, per);
       hipLaunchKernelGGL(k_simple_mfma, dim3((unsigned)np), dim3(256), mlds, s, ext, rec, track_len, pairs + 2 * p0,
-                         prof, wnorm, toff, n2max, np, apply_oti, mpk_g, score_out + p0,
+                         prof, wpad, woff, toff, n2max, np, apply_oti, mpk_g, score_out + p0,
                          oti_out ? oti_out + p0 : nullptr);
       ACOSS_LAUNCH_CHECK();
     }
